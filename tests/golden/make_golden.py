@@ -1,0 +1,198 @@
+"""Generate the committed golden fixtures by running the REFERENCE on CPU, in this container.
+
+    cd tests/golden && python make_golden.py
+
+Only the outputs (.npz / .json under tests/golden/) are committed; the reference itself
+never leaves this container. Weights are deterministic synthetic tensors from
+daclip_amd.synth (no released checkpoint exists offline), loaded into the reference
+modules with strict load_state_dict. Random draws inside the reference sampler
+(torch.randn_like in sde_utils.py:184, 231, 375) are replaced by injected, pre-generated
+noise so the oracle and the HIP path can consume the identical tensors.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(ROOT, "da-clip_amd"))
+
+import _refimport  # noqa: E402
+from daclip_amd import synth  # noqa: E402
+
+torch.set_grad_enabled(False)
+torch.set_num_threads(8)
+ConditionalUNet, open_clip, ref_utils = _refimport.import_reference()
+from open_clip.model import CLIP  # noqa: E402
+from open_clip.daclip_model import DaCLIP  # noqa: E402
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def load(model, seed=0):
+    sd = model.state_dict()
+    spec = {k: tuple(v.shape) for k, v in sd.items()}
+    w = synth.synth_state_dict(spec, seed)
+    model.load_state_dict({k: T(v) for k, v in w.items()}, strict=True)
+    return spec
+
+
+class NoiseInjector:
+    """Replaces torch.randn_like with a queue of pre-generated tensors."""
+
+    def __init__(self, noises):
+        self.q = list(noises)
+        self.orig = torch.randn_like
+
+    def __enter__(self):
+        def fake(x, *a, **k):
+            n = self.q.pop(0)
+            assert tuple(n.shape) == tuple(x.shape), (n.shape, x.shape)
+            return T(n).to(x.dtype)
+        torch.randn_like = fake
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn_like = self.orig
+        assert not self.q, f"{len(self.q)} injected noises unused"
+
+
+def unet_cfg(nf=64):
+    return dict(in_nc=3, out_nc=3, nf=nf, ch_mult=[1, 2, 4, 8], context_dim=512,
+                use_degra_context=True, use_image_context=True)
+
+
+def gen_state_spec():
+    m = ConditionalUNet(**unet_cfg(64))
+    spec = {"unet_nf64": [[k, list(v.shape)] for k, v in m.state_dict().items()]}
+    m32 = ConditionalUNet(**unet_cfg(32))
+    spec["unet_nf32"] = [[k, list(v.shape)] for k, v in m32.state_dict().items()]
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    cfg.pop("custom_text")
+    d = DaCLIP(CLIP(**cfg))
+    spec["daclip_b32"] = [[k, list(v.shape)] for k, v in d.state_dict().items()]
+    with open(os.path.join(HERE, "state_spec.json"), "w") as f:
+        json.dump(spec, f)
+
+
+def gen_unet_forward():
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    load(m, seed=0)
+    for (b, h, w, t, tag) in [(2, 32, 32, 57.0, "32x32"), (1, 30, 34, 3.0, "30x34"),
+                              (1, 64, 64, 100.0, "64x64")]:
+        xt = synth.synth_noise((b, 3, h, w), seed=1, tag="xt" + tag) * 0.3 + 0.5
+        mu = synth.synth_images(b, h, w, seed=2)
+        tc = synth.synth_noise((b, 512), seed=3, tag="text") * 0.5
+        ic = synth.synth_noise((b, 512), seed=4, tag="image") * 0.5
+        out = m(T(xt), T(mu), t, text_context=T(tc), image_context=T(ic)).numpy()
+        np.savez_compressed(os.path.join(HERE, f"unet_fwd_nf64_{tag}.npz"), xt=xt, mu=mu,
+                            t=np.float32(t), text_context=tc, image_context=ic, out=out)
+
+
+def gen_sde():
+    sde = ref_utils.IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005, device="cpu")
+    lin = ref_utils.IRSDE(max_sigma=50, T=100, schedule="linear", eps=0.005, device="cpu")
+    tabs = {}
+    for name, s in (("cos", sde), ("lin", lin)):
+        for f in ("thetas", "sigmas", "thetas_cumsum", "sigma_bars"):
+            tabs[f"{name}_{f}"] = getattr(s, f).numpy()
+        tabs[f"{name}_dt"] = np.float32(s.dt.item())
+    tabs["max_sigma"] = np.float32(sde.max_sigma)
+    np.savez_compressed(os.path.join(HERE, "sde_tables.npz"), **tabs)
+
+    # Full T=100 posterior loop + a 3-step reverse_sde, UNet nf=64 at 16x16, B=1.
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    load(m, seed=0)
+    sde.set_model(m)
+    b, h, w = 1, 16, 16
+    lq = synth.synth_images(b, h, w, seed=7)
+    tc = synth.synth_noise((b, 512), seed=3, tag="text") * 0.5
+    ic = synth.synth_noise((b, 512), seed=4, tag="image") * 0.5
+    n0 = synth.synth_noise((b, 3, h, w), seed=8, tag="noise_state")
+    steps = synth.synth_noise((100, b, 3, h, w), seed=9, tag="steps")
+    with NoiseInjector([n0]):
+        noisy = sde.noise_state(T(lq))
+    sde.set_mu(T(lq))
+    with NoiseInjector(list(steps)):
+        out = sde.reverse_posterior(noisy, text_context=T(tc), image_context=T(ic)).numpy()
+    with NoiseInjector(list(steps[:3])):
+        out_sde = sde.reverse_sde(noisy, T=3, text_context=T(tc), image_context=T(ic)).numpy()
+    out_u8 = ref_utils.tensor2img(T(out.copy()).squeeze())
+    lq_u8 = ref_utils.tensor2img(T(lq.copy()).squeeze())
+    psnr = ref_utils.calculate_psnr(out_u8, lq_u8)
+    np.savez_compressed(os.path.join(HERE, "posterior_loop_16x16.npz"), lq=lq, text_context=tc,
+                        image_context=ic, noise_state=n0, step_noise=steps, noisy=noisy.numpy(),
+                        out=out, out_sde3=out_sde, out_u8=out_u8, lq_u8=lq_u8,
+                        psnr=np.float64(psnr))
+
+
+def _daclip(vision, text, embed):
+    d = DaCLIP(CLIP(embed_dim=embed, vision_cfg=vision, text_cfg=text)).eval()
+    load(d, seed=0)
+    return d
+
+
+def gen_daclip():
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    img = synth.synth_noise((2, 3, 224, 224), seed=11, tag="img4clip")
+    ic, dc = d.encode_image(T(img), control=True)
+    np.savez_compressed(os.path.join(HERE, "daclip_b32_encode.npz"), img=img,
+                        image_context=ic.numpy(), degra_context=dc.numpy())
+    small_v = dict(image_size=64, layers=3, width=128, patch_size=32)
+    small_t = dict(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+    d = _daclip(small_v, small_t, 64)
+    img = synth.synth_noise((3, 3, 64, 64), seed=12, tag="img4clip_small")
+    ic, dc = d.encode_image(T(img), control=True)
+    np.savez_compressed(os.path.join(HERE, "daclip_small_encode.npz"), img=img,
+                        image_context=ic.numpy(), degra_context=dc.numpy())
+
+
+def gen_modules():
+    """Per-module fixtures (small shapes) used to localise kernel bugs."""
+    from models.modules.module_util import ResBlock, LinearAttention, default_conv, NonLinearity
+    from models.modules.attention import SpatialTransformer
+    import functools
+    out = {}
+    rb = functools.partial(ResBlock, conv=default_conv, act=NonLinearity())
+    for tag, din, dout in (("rb64", 64, 64), ("rb96_32", 96, 32)):
+        m = rb(dim_in=din, dim_out=dout, time_emb_dim=256).eval()
+        load(m, seed=5)
+        x = synth.synth_noise((2, din, 12, 10), seed=13, tag=tag)
+        te = synth.synth_noise((2, 256), seed=14, tag=tag + "t")
+        out[f"{tag}_x"], out[f"{tag}_t"] = x, te
+        out[f"{tag}_y"] = m(T(x), T(te)).numpy()
+    la = LinearAttention(64).eval()
+    load(la, seed=5)
+    x = synth.synth_noise((2, 64, 16, 12), seed=15, tag="la")
+    out["la_x"], out["la_y"] = x, la(T(x)).numpy()
+    st = SpatialTransformer(64, 2, 32, depth=1, context_dim=512).eval()
+    load(st, seed=5)
+    x = synth.synth_noise((2, 64, 8, 8), seed=16, tag="st")
+    c = synth.synth_noise((2, 1, 512), seed=17, tag="stc")
+    out["st_x"], out["st_c"], out["st_y"] = x, c, st(T(x), context=T(c)).numpy()
+    np.savez_compressed(os.path.join(HERE, "modules.npz"), **out)
+
+
+def gen_img_metrics():
+    a = synth.synth_images(1, 24, 20, seed=21)[0]
+    b = np.clip(a + 0.03 * synth.synth_noise(a.shape, seed=22, tag="pert"), -0.1, 1.1)
+    ua = ref_utils.tensor2img(T(a.copy()))
+    ub = ref_utils.tensor2img(T(b.copy()))
+    np.savez_compressed(os.path.join(HERE, "img_metrics.npz"), a=a, b=b, ua=ua, ub=ub,
+                        psnr=np.float64(ref_utils.calculate_psnr(ua, ub)))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "modules", "img"]
+    fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
+               modules=gen_modules, img=gen_img_metrics)
+    for w in which:
+        print("generating", w, flush=True)
+        fns[w]()

@@ -1,0 +1,88 @@
+"""Pin the numpy oracle against fixtures produced by the reference itself (make_golden.py)."""
+import numpy as np
+import pytest
+
+import oracle
+from oracle import unet as OU, clip as OC, sde as OS, imgs as OI
+
+
+def rel(a, b):
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+@pytest.mark.parametrize("tag", ["32x32", "30x34", "64x64"])
+def test_unet_forward_matches_reference(golden, unet_sd, tag):
+    g = golden(f"unet_fwd_nf64_{tag}.npz")
+    out = OU.forward(unet_sd, g["xt"], g["mu"], float(g["t"]), g["text_context"], g["image_context"])
+    assert out.shape == g["out"].shape
+    assert rel(out, g["out"]) < 2e-5
+
+
+def test_modules_match_reference(golden):
+    from daclip_amd import synth
+    g = golden("modules.npz")
+    for tag in ("rb64", "rb96_32"):
+        din = g[f"{tag}_x"].shape[1]
+        dout = g[f"{tag}_y"].shape[1]
+        spec = {"mlp.1.weight": (2 * dout, 256), "mlp.1.bias": (2 * dout,),
+                "block1.proj.weight": (dout, din, 3, 3), "block2.proj.weight": (dout, dout, 3, 3)}
+        if din != dout:
+            spec["res_conv.weight"] = (dout, din, 1, 1)
+        sd = synth.synth_state_dict(spec, seed=5)
+        y = OU.resblock(sd, "", g[f"{tag}_x"], g[f"{tag}_t"])
+        assert rel(y, g[f"{tag}_y"]) < 1e-5, tag
+    spec = {"to_qkv.weight": (384, 64, 1, 1), "to_out.0.weight": (64, 128, 1, 1),
+            "to_out.0.bias": (64,), "to_out.1.g": (1, 64, 1, 1)}
+    sd = synth.synth_state_dict(spec, seed=5)
+    assert rel(OU.linear_attention(sd, "", g["la_x"]), g["la_y"]) < 1e-5
+
+
+def test_sde_tables_match_reference(golden):
+    g = golden("sde_tables.npz")
+    for name, sched in (("cos", "cosine"), ("lin", "linear")):
+        s = OS.IRSDE(50, 100, sched, 0.005)
+        for f in ("thetas", "sigmas", "thetas_cumsum", "sigma_bars"):
+            np.testing.assert_allclose(getattr(s, f), g[f"{name}_{f}"], rtol=1e-5, atol=1e-6)  # cos: 1-ulp libm differences
+        np.testing.assert_allclose(s.dt, g[f"{name}_dt"], rtol=2e-6)
+    assert s.max_sigma == pytest.approx(float(g["max_sigma"]))
+
+
+def test_posterior_loop_matches_reference(golden, unet_sd):
+    """Full T=100 posterior loop at 16x16 with injected noise (parity of the whole sampler)."""
+    g = golden("posterior_loop_16x16.npz")
+    s = OS.IRSDE(50, 100, "cosine", 0.005)
+    s.mu = g["lq"]
+    s.model = lambda x, mu, t, **k: OU.forward(unet_sd, x, mu, t, **k)
+    noisy = s.noise_state(g["lq"], g["noise_state"])
+    np.testing.assert_allclose(noisy, g["noisy"], rtol=1e-6, atol=1e-7)
+    ctx = dict(text_context=g["text_context"], image_context=g["image_context"])
+    out = s.reverse_posterior(noisy, g["step_noise"], **ctx)
+    assert rel(out, g["out"]) < 1e-3
+    u8 = OI.tensor2img(out[0])
+    assert np.mean(u8 != g["out_u8"]) < 0.01
+    out3 = s.reverse_sde(noisy, g["step_noise"][:3], T=3, **ctx)
+    assert rel(out3, g["out_sde3"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["daclip_small_encode.npz", "daclip_b32_encode.npz"])
+def test_daclip_encode_matches_reference(golden, name):
+    from daclip_amd import arch, synth
+    g = golden(name)
+    if "small" in name:
+        v = arch.VisionConfig(image_size=64, patch_size=32, width=128, layers=3, embed_dim=64)
+        t = arch.TextConfig(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+    else:
+        v, t = arch.VIT_B_32, arch.TEXT_B_32
+    spec = {k: s for k, s in arch.daclip_state_spec(v, t).items()
+            if "visual" in k}
+    sd = synth.synth_state_dict(spec, seed=0)
+    ic, dc = OC.encode_image(sd, g["img"])
+    assert rel(ic, g["image_context"]) < 1e-4
+    assert rel(dc, g["degra_context"]) < 1e-4
+
+
+def test_img_metrics_match_reference(golden):
+    g = golden("img_metrics.npz")
+    assert np.array_equal(OI.tensor2img(g["a"]), g["ua"])
+    assert np.array_equal(OI.tensor2img(g["b"]), g["ub"])
+    assert OI.calculate_psnr(g["ua"], g["ub"]) == pytest.approx(float(g["psnr"]), abs=1e-12)
