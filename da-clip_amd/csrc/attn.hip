@@ -1,0 +1,212 @@
+// attn.hip — self-attention kernels.
+//
+// flash_attn_d32: SpatialTransformer self-attention (attention.py:170-193: heads = C/32,
+// d_head = 32, L = (H/8)*(W/8) tokens). Flash-style, one workgroup = 64 queries of one
+// (image, head), 4 waves x 16 queries, key tiles of 64 through LDS, online softmax in fp32.
+// Computed transposed: S^T = K Q^T (A = K rows from LDS, B = this wave's 16 queries held in
+// registers) and O^T = V^T P^T. Because the S^T accumulator keeps keys in registers and
+// queries on lanes, P^T feeds the second MFMA straight from registers: the k order inside a
+// step is permuted identically for V^T (read from LDS in that order), so no LDS round trip
+// for P is needed.
+//
+// small_mha: nn.MultiheadAttention core of the ViT blocks (transformer.py:203, 217-230):
+// L = 50 (B/32) tokens, 12 heads x 64; tiny, one workgroup per (image, head), fp32 math.
+#include "common.h"
+#include "kernels.h"
+
+namespace dac {
+
+template <typename T>
+__global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qkv, T* o, int L,
+                                                        int H, float scale) {
+  constexpr int D = 32;
+  constexpr int KT = 64;                     // keys per tile
+  constexpr int ES = sizeof(T);
+  constexpr int KROW = D * ES + 16;          // padded K row (bytes)
+  constexpr int VROW = KT * ES + 16;         // padded V^T row (bytes)
+  constexpr int KSTEP = Mma<T>::KSTEP;
+  __shared__ __attribute__((aligned(16))) char sK[KT * KROW];
+  __shared__ __attribute__((aligned(16))) char sV[D * VROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int ld = 3 * H * D;
+  const T* base = qkv + (size_t)b * L * ld;
+  const int q = blockIdx.x * 64 + wave * 16 + lr;
+
+  // Q fragments (B operand of S^T = K Q^T): column = query, k = d.
+  u32x4 qf[D / KSTEP];
+#pragma unroll
+  for (int s = 0; s < D / KSTEP; ++s) {
+    const int d0 = s * KSTEP + lg * (KSTEP / 4);
+    qf[s] = q < L ? *reinterpret_cast<const u32x4*>(base + (size_t)q * ld + h * D + d0)
+                  : u32x4{0u, 0u, 0u, 0u};
+  }
+
+  f32x4 oacc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
+  float mrun = -INFINITY, lrun = 0.f;
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int NVEC = KT * D / VE;          // 16-byte vectors per K (or V) tile
+
+  for (int k0 = 0; k0 < L; k0 += KT) {
+    __syncthreads();
+    for (int v = tid; v < NVEC; v += 256) {
+      const int key = v / (D / VE), dv = (v % (D / VE)) * VE;
+      const int kk = k0 + key;
+      u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+      if (kk < L) {
+        kv = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + H * D + h * D + dv);
+        vv = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + 2 * H * D + h * D + dv);
+      }
+      *reinterpret_cast<u32x4*>(sK + key * KROW + dv * ES) = kv;
+      const T* ve = reinterpret_cast<const T*>(&vv);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) *reinterpret_cast<T*>(sV + (dv + e) * VROW + key * ES) = ve[e];
+    }
+    __syncthreads();
+
+    // S^T tile: 4 m-subtiles of 16 keys x this wave's 16 queries.
+    f32x4 s[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      s[mi] = f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int ks = 0; ks < D / KSTEP; ++ks) {
+        const int d0 = ks * KSTEP + lg * (KSTEP / 4);
+        const u32x4 ka = *reinterpret_cast<const u32x4*>(sK + (mi * 16 + lr) * KROW + d0 * ES);
+        Mma<T>::run(s[mi], ka, qf[ks]);
+      }
+    }
+    // Online softmax over keys for this lane's query column.
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + mi * 16 + lg * 4 + r;
+        const float v = key < L ? s[mi][r] * scale : -INFINITY;
+        s[mi][r] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mnew = fmaxf(mrun, tmax);
+    const float corr = expf(mrun - mnew);
+    float psum = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = expf(s[mi][r] - mnew);
+        s[mi][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16, 64);
+    psum += __shfl_xor(psum, 32, 64);
+    lrun = lrun * corr + psum;
+    mrun = mnew;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) oacc[i] *= corr;
+
+    // O^T += V^T P^T over the 64 keys.
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {           // k-step = 32 keys = subtiles 2st, 2st+1
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (bf16)s[2 * st][j];
+          pb[4 + j] = (bf16)s[2 * st + 1][j];
+        }
+        const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          const char* row = sV + (mi * 16 + lr) * VROW;
+          uint2 lo = *reinterpret_cast<const uint2*>(row + (st * 32 + lg * 4) * ES);
+          uint2 hi = *reinterpret_cast<const uint2*>(row + (st * 32 + 16 + lg * 4) * ES);
+          Mma<T>::run(oacc[mi], u32x4{lo.x, lo.y, hi.x, hi.y}, pbu);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {           // k-step = 16 keys = subtile st
+        const u32x4 pbu = __builtin_bit_cast(u32x4, s[st]);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          const u32x4 va = *reinterpret_cast<const u32x4*>(sV + (mi * 16 + lr) * VROW +
+                                                           (st * 16 + lg * 4) * ES);
+          Mma<T>::run(oacc[mi], va, pbu);
+        }
+      }
+    }
+  }
+  if (q >= L) return;
+  const float inv = 1.f / lrun;
+  T* out = o + ((size_t)b * L + q) * (H * D) + h * D;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[mi * 16 + lg * 4 + r] = from_f<T>(oacc[mi][r] * inv);
+}
+
+template <typename T>
+void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
+  dim3 g((L + 63) / 64, H, B);
+  flash_d32_kernel<T><<<g, 256, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+}
+
+// ------------------------------------------------------------------------------ small MHA
+template <typename T>
+__global__ void __launch_bounds__(64) small_mha_kernel(const T* __restrict__ qkv, T* o, int L,
+                                                       int H, int D) {
+  extern __shared__ float sm[];               // K [L][D+1], V [L][D]
+  const int b = blockIdx.y, h = blockIdx.x;
+  const int ld = 3 * H * D;
+  const T* base = qkv + (size_t)b * L * ld;
+  float* sk = sm;
+  float* sv = sm + L * (D + 1);
+  for (int i = threadIdx.x; i < L * D; i += 64) {
+    const int t = i / D, d = i - t * D;
+    sk[t * (D + 1) + d] = to_f(base[(size_t)t * ld + H * D + h * D + d]);
+    sv[t * D + d] = to_f(base[(size_t)t * ld + 2 * H * D + h * D + d]);
+  }
+  __syncthreads();
+  const float scale = rsqrtf((float)D);
+  for (int qi = threadIdx.x; qi < L; qi += 64) {
+    float qv[64];
+    for (int d = 0; d < D; ++d) qv[d] = to_f(base[(size_t)qi * ld + h * D + d]) * scale;
+    float sc[64];
+    float mx = -INFINITY;
+    for (int t = 0; t < L; ++t) {
+      float a = 0.f;
+      for (int d = 0; d < D; ++d) a += qv[d] * sk[t * (D + 1) + d];
+      sc[t] = a;
+      mx = fmaxf(mx, a);
+    }
+    float sum = 0.f;
+    for (int t = 0; t < L; ++t) { sc[t] = expf(sc[t] - mx); sum += sc[t]; }
+    const float inv = 1.f / sum;
+    T* out = o + ((size_t)b * L + qi) * (H * D) + h * D;
+    for (int d = 0; d < D; ++d) {
+      float a = 0.f;
+      for (int t = 0; t < L; ++t) a += sc[t] * sv[t * D + d];
+      out[d] = from_f<T>(a * inv);
+    }
+  }
+}
+
+template <typename T>
+void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t st) {
+  const size_t smem = (size_t)L * (2 * D + 1) * sizeof(float);
+  small_mha_kernel<T><<<dim3(H, B), 64, smem, st>>>((const T*)qkv, (T*)o, L, H, D);
+}
+
+#define INST(T)                                                                           \
+  template void flash_attn_d32<T>(const void*, void*, int, int, int, float, hipStream_t); \
+  template void small_mha<T>(const void*, void*, int, int, int, int, hipStream_t);
+INST(float)
+INST(bf16)
+#undef INST
+
+}  // namespace dac

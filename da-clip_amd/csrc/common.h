@@ -1,0 +1,89 @@
+// common.h — shared device helpers for the gfx950 kernels of libdaclip_hip.
+//
+// Storage/compute types: `float` (parity mode, exact-f32 MFMA v_mfma_f32_16x16x4_f32) and
+// `bf16` (perf mode, v_mfma_f32_16x16x32_bf16, fp32 accumulate). Every tile operand is
+// read from LDS as one 16-byte vector per lane, so one kernel body serves both types:
+// a 16-byte vector holds VE = 16/sizeof(T) elements (8 bf16 or 4 f32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define DEV __device__ __forceinline__
+
+template <typename T> struct TypeInfo;
+template <> struct TypeInfo<float> { static constexpr int VE = 4; };
+template <> struct TypeInfo<bf16> { static constexpr int VE = 8; };
+
+DEV float to_f(float v) { return v; }
+DEV float to_f(bf16 v) { return (float)v; }
+template <typename T> DEV T from_f(float v);
+template <> DEV float from_f<float>(float v) { return v; }
+template <> DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+
+// Load / store VE elements (16 bytes) as fp32 values.
+template <typename T> DEV void load_vec(const T* p, float* out);
+template <> DEV void load_vec<float>(const float* p, float* out) {
+  f32x4 v = *reinterpret_cast<const f32x4*>(p);
+  out[0] = v[0]; out[1] = v[1]; out[2] = v[2]; out[3] = v[3];
+}
+template <> DEV void load_vec<bf16>(const bf16* p, float* out) {
+  bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = (float)v[i];
+}
+template <typename T> DEV void store_vec(T* p, const float* in);
+template <> DEV void store_vec<float>(float* p, const float* in) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{in[0], in[1], in[2], in[3]};
+}
+template <> DEV void store_vec<bf16>(bf16* p, const float* in) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (bf16)in[i];
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+// ---------------------------------------------------------------------------------------
+// MFMA 16x16 tile step. acc(16x16) += A(16 x KSTEP) * B(KSTEP x 16), where lane l supplies
+// 16 bytes of row (l&15) of A (resp. column (l&15) of B stored n-major) at k-offset
+// KSTEP/4 * (l>>4) elements. For bf16 one v_mfma_f32_16x16x32_bf16 consumes the vector.
+// For f32 the 4 floats feed 4 v_mfma_f32_16x16x4_f32 (element j of lane group g is
+// k = 4g + j): any k-permutation shared by A and B leaves the sum unchanged, so the result
+// is an exact-f32 dot product over the same 16 k values.
+// C layout (both): acc[r] = C[row = 4*(l>>4) + r][col = l&15].
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  static constexpr int KSTEP = 32;
+  DEV static void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static constexpr int KSTEP = 16;
+  DEV static void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], acc, 0, 0, 0);
+  }
+};
+
+DEV float silu_f(float x) { return x / (1.f + expf(-x)); }
+DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

@@ -1,0 +1,1021 @@
+// engine.cpp — network executors of libdaclip_hip (host C++, launches the gfx950 kernels).
+//
+// ConditionalUNet forward: DenoisingUNet_arch.py:118-174 (blocks: module_util.py:100-185,
+//   attention.py:152-261). DaCLIP.encode_image(control=True): daclip_model.py:46-53,
+//   transformer.py:288-369, 507-555. IR-SDE: utils/sde_utils.py:91-313.
+// All activations are NHWC in the compute dtype T; every conv/linear goes through conv_call
+// (MFMA implicit GEMM) with its elementwise tail fused into the epilogue.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace dac {
+
+// ============================================================================= weights
+const HostW* WStore::get(const std::string& key, std::vector<int64_t> shape) {
+  auto it = m.find(key);
+  if (it == m.end()) {
+    missing.push_back(key);
+    return nullptr;
+  }
+  if (it->second.shape != shape) {
+    std::string a, b;
+    for (auto s : shape) a += std::to_string(s) + ",";
+    for (auto s : it->second.shape) b += std::to_string(s) + ",";
+    throw Error(DAC_E_KEY, "size mismatch for " + key + ": expected [" + a + "] got [" + b + "]");
+  }
+  it->second.used = true;
+  return &it->second;
+}
+
+DevPool::~DevPool() {
+  for (void* p : ptrs) (void)hipFree(p);
+}
+void* DevPool::alloc(size_t bytes) {
+  void* p = nullptr;
+  HIP_OK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  ptrs.push_back(p);
+  return p;
+}
+void* DevPool::upload(const void* host, size_t bytes) {
+  void* p = alloc(bytes);
+  HIP_OK(hipMemcpy(p, host, bytes, hipMemcpyHostToDevice));
+  return p;
+}
+
+uint16_t f2bf_host(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T>
+struct Packer {
+  DevPool& pool;
+  WStore& ws;
+  static constexpr int VE = sizeof(T) == 2 ? 8 : 4;
+
+  const void* upload_T(const std::vector<float>& v) {
+    if (sizeof(T) == 4) return pool.upload(v.data(), v.size() * 4);
+    std::vector<uint16_t> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host(v[i]);
+    return pool.upload(h.data(), h.size() * 2);
+  }
+  const float* f32(const std::string& key, std::vector<int64_t> shape) {
+    const HostW* w = ws.get(key, shape);
+    if (!w) return nullptr;
+    return (const float*)pool.upload(w->v.data(), w->v.size() * 4);
+  }
+  // [I][O] -> [O][I] fp32 (for `pooled @ proj`).
+  const float* f32_t(const std::string& key, int I, int O) {
+    const HostW* w = ws.get(key, {I, O});
+    if (!w) return nullptr;
+    std::vector<float> t((size_t)I * O);
+    for (int i = 0; i < I; ++i)
+      for (int o = 0; o < O; ++o) t[(size_t)o * I + i] = w->v[(size_t)i * O + o];
+    return (const float*)pool.upload(t.data(), t.size() * 4);
+  }
+  static int pad_to(int c, int v) { return (c + v - 1) / v * v; }
+  // conv weight [O][C][kh][kw] (4-D key) or linear [O][C] (2-D key, kh = kw = 1).
+  ConvW conv(const std::string& key, int O, int C, int kh, int kw, const std::string& bkey = "",
+             bool linear2d = false) {
+    ConvW cw;
+    cw.cout = O; cw.cin_real = C; cw.cin = pad_to(C, VE); cw.kh = kh; cw.kw = kw;
+    const HostW* w = linear2d ? ws.get(key, {O, C}) : ws.get(key, {O, C, kh, kw});
+    if (!bkey.empty()) cw.b = f32(bkey, {O});
+    if (!w) return cw;
+    std::vector<float> p((size_t)O * kh * kw * cw.cin, 0.f);
+    for (int o = 0; o < O; ++o)
+      for (int c = 0; c < C; ++c)
+        for (int y = 0; y < kh; ++y)
+          for (int x = 0; x < kw; ++x)
+            p[(((size_t)o * kh + y) * kw + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
+    cw.w = upload_T(p);
+    return cw;
+  }
+  ConvW linear(const std::string& key, int O, int I, const std::string& bkey = "") {
+    return conv(key, O, I, 1, 1, bkey, true);
+  }
+  // Row-concatenation of several [Oi][I] linears (q | k | v) into one GEMM.
+  ConvW concat(const std::vector<std::string>& keys, int O, int I) {
+    ConvW cw;
+    cw.cout = O * (int)keys.size(); cw.cin = cw.cin_real = I;
+    std::vector<float> p;
+    bool ok = true;
+    for (auto& k : keys) {
+      const HostW* w = ws.get(k, {O, I});
+      if (!w) { ok = false; continue; }
+      p.insert(p.end(), w->v.begin(), w->v.end());
+    }
+    if (ok) cw.w = upload_T(p);
+    return cw;
+  }
+  // GEGLU proj [2F][I] (+bias): rows reordered so each 32-row group holds 16 "x" rows then
+  // their 16 "gate" rows; the conv epilogue pairs accumulator tiles j, j+1.
+  ConvW geglu(const std::string& key, const std::string& bkey, int F, int I) {
+    ConvW cw;
+    cw.cout = 2 * F; cw.cin = cw.cin_real = I;
+    const HostW* w = ws.get(key, {2 * F, I});
+    const HostW* b = ws.get(bkey, {2 * F});
+    if (!w || !b) return cw;
+    std::vector<float> p((size_t)2 * F * I), pb(2 * F);
+    for (int r = 0; r < 2 * F; ++r) {
+      const int g = r / 32, s = r % 32;
+      const int src = s < 16 ? 16 * g + s : F + 16 * g + (s - 16);
+      std::copy(w->v.begin() + (size_t)src * I, w->v.begin() + (size_t)(src + 1) * I,
+                p.begin() + (size_t)r * I);
+      pb[r] = b->v[src];
+    }
+    cw.w = upload_T(p);
+    cw.b = (const float*)pool.upload(pb.data(), pb.size() * 4);
+    return cw;
+  }
+};
+
+// ============================================================================= launches
+int conv_tile_id(int cout, int act) {
+  if (cout <= 16 && act != ACT_GEGLU) return 0;
+  if (cout <= 64) return 1;
+  return 2;
+}
+
+Profiler::~Profiler() {
+  for (auto e : ev) (void)hipEventDestroy(e);
+}
+
+template <typename T>
+void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,
+               int B, int Hs, int Ws, int up, int stride, int pad, void* y, int ldy,
+               const Epi& e) {
+  ConvArgs a{};
+  a.x1 = x1; a.x2 = x2; a.ld1 = ld1; a.ld2 = ld2; a.C1 = C1; a.Cin = cw.cin;
+  a.Hs = Hs; a.Ws = Ws; a.up = up; a.B = B;
+  const int Hin = up ? 2 * Hs : Hs, Win = up ? 2 * Ws : Ws;
+  a.Ho = (Hin + 2 * pad - cw.kh) / stride + 1;
+  a.Wo = (Win + 2 * pad - cw.kw) / stride + 1;
+  a.Cout = cw.cout; a.K = cw.kh * cw.kw * cw.cin; a.w = cw.w; a.bias = cw.b;
+  a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
+  a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
+  const double M = (double)B * a.Ho * a.Wo;
+  const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
+  r.flops += fl;
+  Profiler* p = r.prof;
+  const bool timed = p && p->kernel_id == cw.kh * 100 + conv_tile_id(cw.cout, e.act);
+  if (r.dry) {
+    if (timed) p->used++;
+    return;
+  }
+  if (!cw.w) throw Error(DAC_E_STATE, "conv weight not loaded");
+  if (a.Cin % (16 / (int)sizeof(T)) || (x2 == nullptr && C1 < a.Cin))
+    throw Error(DAC_E_ARG, "conv: bad channel layout");
+  if (timed) {
+    if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
+    HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
+  }
+  conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+  if (timed) {
+    HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
+    p->used++;
+    p->launches++;
+    p->flops += fl;
+    // Algorithmic HBM bytes: every operand touched once (input, weights, output, residuals).
+    const double es = sizeof(T);
+    p->bytes += es * ((double)B * Hs * Ws * cw.cin_real + (double)cw.cout * cw.kh * cw.kw * cw.cin +
+                      M * cw.cout * (1 + (e.res1 ? 1 : 0) + (e.res2 ? 1 : 0)));
+  }
+}
+
+template <typename T>
+static void ln(Run& r, const void* x, int ldx, void* y, int ldy, const void* res, int ldr,
+               const float* g, const float* b, int rows, int C, float eps) {
+  if (r.dry) return;
+  layernorm<T>(x, ldx, y, ldy, res, ldr, g, b, rows, C, eps, r.st);
+}
+
+// ============================================================================= schedule
+void compute_schedule(SdeSchedule& s, float max_sigma, int T, int schedule, float eps) {
+  // sde_utils.py:84-154 in fp32 (torch 0-dim / 1-D float32 semantics).
+  const double ms = max_sigma >= 1 ? max_sigma / 255.0 : max_sigma;
+  s.T = T;
+  s.max_sigma = (float)ms;
+  const int n = T + 1;
+  s.thetas.assign(n, 0.f);
+  if (schedule == DAC_COSINE) {
+    const int ts = T + 2;
+    std::vector<float> ac(ts + 1);
+    const float c1 = (float)0.008, c2 = (float)(1 + 0.008), c3 = (float)(M_PI * 0.5);
+    for (int i = 0; i <= ts; ++i) {
+      const float x = (float)i;
+      const float c = std::cos(((x / (float)ts) + c1) / c2 * c3);
+      ac[i] = c * c;
+    }
+    const float a0 = ac[0];
+    for (int i = 0; i <= ts; ++i) ac[i] = ac[i] / a0;
+    for (int i = 0; i < n; ++i) s.thetas[i] = 1.f - ac[i + 1];
+  } else if (schedule == DAC_LINEAR) {
+    const double scale = 1000.0 / n;
+    const float b0 = (float)(scale * 0.0001), b1 = (float)(scale * 0.02);
+    for (int i = 0; i < n; ++i)
+      s.thetas[i] = n == 1 ? b0 : b0 + (b1 - b0) * (float)i / (float)(n - 1);
+  } else {
+    for (int i = 0; i < n; ++i) s.thetas[i] = 1.f;
+  }
+  s.sigmas.resize(n);
+  s.tcum.resize(n);
+  s.sbar.resize(n);
+  const float ms2x2 = (float)(ms * ms * 2), ms2 = (float)(ms * ms);
+  float acc = 0.f;
+  for (int i = 0; i < n; ++i) {
+    s.sigmas[i] = std::sqrt(ms2x2 * s.thetas[i]);
+    acc += s.thetas[i];
+    s.tcum[i] = acc - s.thetas[0];
+  }
+  s.dt = (-1.f / s.tcum[n - 1]) * (float)std::log((double)eps);
+  for (int i = 0; i < n; ++i) s.sbar[i] = std::sqrt(ms2 * (1.f - std::exp(-2.f * s.tcum[i] * s.dt)));
+}
+
+StepCoef SdeSchedule::coef(int t, int mode) const {
+  (void)mode;
+  StepCoef c{};
+  const float th = thetas[t], tc = tcum[t], tc1 = tcum[t - 1];
+  c.sbar = sbar[t];
+  c.ea = std::exp(tc * dt);                                  // sde_utils.py:246
+  const float A = std::exp(-th * dt), B = std::exp(-tc * dt), C = std::exp(-tc1 * dt);
+  c.t1 = A * (1.f - C * C) / (1.f - B * B);                  // :210
+  c.t2 = C * (1.f - A * A) / (1.f - B * B);                  // :211
+  const float A2 = std::exp(-2.f * th * dt), B2 = std::exp(-2.f * tc * dt),
+              C2 = std::exp(-2.f * tc1 * dt);
+  const float var = (1.f - A2) * (1.f - C2) / (1.f - B2);    // :220
+  const float lv = std::log(std::max(var, 1e-20f * dt));     // :223-224
+  c.std = std::exp(0.5f * lv) * max_sigma;                   // :225
+  c.theta = th;
+  c.sigma2 = sigmas[t] * sigmas[t];
+  c.dt = dt;
+  c.sigma_sqrt_dt = sigmas[t] * (float)std::sqrt((double)dt);
+  return c;
+}
+
+// ============================================================================= UNet
+template <typename T>
+struct UNetNet {
+  struct RB { ConvW c1, c2, res; bool has_res = false; int din = 0, dout = 0;
+              const float* mw = nullptr; const float* mb = nullptr; int ss_off = 0; };
+  struct LA { const float* gpre = nullptr; ConvW qkv, out; const float* gout = nullptr; };
+  struct ST { const float* gpre = nullptr; const float *gnw = nullptr, *gnb = nullptr;
+              ConvW pin; const float *n1w = nullptr, *n1b = nullptr, *n3w = nullptr, *n3b = nullptr;
+              ConvW qkv, o, ff1, ff2, pout; const float *a2v = nullptr, *a2o = nullptr, *a2ob = nullptr;
+              int cc_off = 0; };
+  struct Attn { bool st = false; LA la; ST s; };
+  struct Level { RB b1, b2; Attn at; ConvW samp; };
+
+  dac_config cfg;
+  int nf, depth, tdim, ctx;
+  bool degra, imgctx;
+  std::vector<std::pair<int, int>> levels;
+  ConvW init_conv, final_conv;
+  const float *tm1w, *tm1b, *tm3w, *tm3b, *prompt = nullptr, *t0w = nullptr, *t0b = nullptr,
+              *t2w = nullptr, *t2b = nullptr, *pmw = nullptr, *pmb = nullptr;
+  std::vector<Level> downs, ups;
+  RB mid1, mid2, fin;
+  Attn mid_attn;
+  int ss_total = 0, cc_total = 0, n_st = 0;
+
+  explicit UNetNet(const dac_config& c) : cfg(c) {
+    nf = c.nf; depth = c.depth; tdim = nf * 4; ctx = c.context_dim;
+    degra = ctx > 0 && c.use_degra_context;
+    imgctx = ctx > 0 && c.use_image_context;
+    std::vector<int> m = {1};
+    for (int i = 0; i < depth; ++i) m.push_back(c.ch_mult[i]);
+    for (int i = 0; i < depth; ++i) levels.push_back({nf * m[i], nf * m[i + 1]});
+  }
+
+  RB load_rb(Packer<T>& P, const std::string& p, int din, int dout) {
+    RB rb;
+    rb.din = din; rb.dout = dout;
+    rb.mw = P.f32(p + "mlp.1.weight", {2 * dout, tdim});
+    rb.mb = P.f32(p + "mlp.1.bias", {2 * dout});
+    rb.c1 = P.conv(p + "block1.proj.weight", dout, din, 3, 3);
+    rb.c2 = P.conv(p + "block2.proj.weight", dout, dout, 3, 3);
+    if (din != dout) {
+      rb.has_res = true;
+      rb.res = P.conv(p + "res_conv.weight", dout, din, 1, 1);
+    }
+    rb.ss_off = ss_total;
+    ss_total += 2 * dout;
+    return rb;
+  }
+  Attn load_attn(Packer<T>& P, const std::string& p, int C, bool st) {
+    Attn a;
+    a.st = st;
+    const std::string f = p + "fn.fn.";
+    if (!st) {
+      a.la.gpre = P.f32(p + "fn.norm.g", {1, C, 1, 1});
+      a.la.qkv = P.conv(f + "to_qkv.weight", 384, C, 1, 1);
+      a.la.out = P.conv(f + "to_out.0.weight", C, 128, 1, 1, f + "to_out.0.bias");
+      a.la.gout = P.f32(f + "to_out.1.g", {1, C, 1, 1});
+      return a;
+    }
+    ST& s = a.s;
+    s.gpre = P.f32(p + "fn.norm.g", {1, C, 1, 1});
+    s.gnw = P.f32(f + "norm.weight", {C});
+    s.gnb = P.f32(f + "norm.bias", {C});
+    s.pin = P.conv(f + "proj_in.weight", C, C, 1, 1, f + "proj_in.bias");
+    const std::string b = f + "transformer_blocks.0.";
+    s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C);
+    s.o = P.linear(b + "attn1.to_out.0.weight", C, C, b + "attn1.to_out.0.bias");
+    s.ff1 = P.geglu(b + "ff.net.0.proj.weight", b + "ff.net.0.proj.bias", 4 * C, C);
+    s.ff2 = P.linear(b + "ff.net.2.weight", C, 4 * C, b + "ff.net.2.bias");
+    // attn2 attends to ONE context token: softmax over a single key is exactly 1, so its
+    // output is to_out(to_v(ctx)) for every query; to_q / to_k / norm2 cannot affect it
+    // (attention.py:170-193 with context [B,1,ctx]). They are still required keys.
+    (void)P.f32(b + "attn2.to_q.weight", {C, C});
+    (void)P.f32(b + "attn2.to_k.weight", {C, ctx});
+    s.a2v = P.f32(b + "attn2.to_v.weight", {C, ctx});
+    s.a2o = P.f32(b + "attn2.to_out.0.weight", {C, C});
+    s.a2ob = P.f32(b + "attn2.to_out.0.bias", {C});
+    s.n1w = P.f32(b + "norm1.weight", {C});
+    s.n1b = P.f32(b + "norm1.bias", {C});
+    (void)P.f32(b + "norm2.weight", {C});
+    (void)P.f32(b + "norm2.bias", {C});
+    s.n3w = P.f32(b + "norm3.weight", {C});
+    s.n3b = P.f32(b + "norm3.bias", {C});
+    s.pout = P.conv(f + "proj_out.weight", C, C, 1, 1, f + "proj_out.bias");
+    s.cc_off = cc_total;
+    cc_total += C;
+    n_st++;
+    return a;
+  }
+
+  void load(Packer<T>& P) {
+    ss_total = cc_total = n_st = 0;
+    if (degra) prompt = P.f32("prompt", {1, tdim});
+    init_conv = P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7);
+    tm1w = P.f32("time_mlp.1.weight", {tdim, nf});
+    tm1b = P.f32("time_mlp.1.bias", {tdim});
+    tm3w = P.f32("time_mlp.3.weight", {tdim, tdim});
+    tm3b = P.f32("time_mlp.3.bias", {tdim});
+    if (degra) {
+      t0w = P.f32("text_mlp.0.weight", {tdim, ctx});
+      t0b = P.f32("text_mlp.0.bias", {tdim});
+      t2w = P.f32("text_mlp.2.weight", {tdim, tdim});
+      t2b = P.f32("text_mlp.2.bias", {tdim});
+      pmw = P.f32("prompt_mlp.weight", {tdim, tdim});
+      pmb = P.f32("prompt_mlp.bias", {tdim});
+    }
+    downs.assign(depth, Level());
+    ups.assign(depth, Level());
+    for (int i = 0; i < depth; ++i) {
+      const auto [din, dout] = levels[i];
+      const std::string p = "downs." + std::to_string(i) + ".";
+      Level& L = downs[i];
+      L.b1 = load_rb(P, p + "0.", din, din);
+      L.b2 = load_rb(P, p + "1.", din, din);
+      L.at = load_attn(P, p + "2.", din, imgctx && i >= 3);
+      L.samp = i != depth - 1 ? P.conv(p + "3.weight", dout, din, 4, 4, p + "3.bias")
+                              : P.conv(p + "3.weight", dout, din, 3, 3);
+    }
+    for (int j = 0; j < depth; ++j) {
+      const int i = depth - 1 - j;
+      const auto [din, dout] = levels[i];
+      const std::string p = "ups." + std::to_string(j) + ".";
+      Level& L = ups[j];
+      L.b1 = load_rb(P, p + "0.", dout + din, dout);
+      L.b2 = load_rb(P, p + "1.", dout + din, dout);
+      L.at = load_attn(P, p + "2.", dout, imgctx && i >= 3);
+      L.samp = i != 0 ? P.conv(p + "3.1.weight", din, dout, 3, 3, p + "3.1.bias")
+                      : P.conv(p + "3.weight", din, dout, 3, 3);
+    }
+    const int mid = levels.back().second;
+    mid1 = load_rb(P, "mid_block1.", mid, mid);
+    mid_attn = load_attn(P, "mid_attn.", mid, imgctx);
+    mid2 = load_rb(P, "mid_block2.", mid, mid);
+    fin = load_rb(P, "final_res_block.", 2 * nf, nf);
+    final_conv = P.conv("final_conv.weight", cfg.out_nc, nf, 3, 3, "final_conv.bias");
+  }
+
+  // ----------------------------------------------------------------- per-call tables
+  // ss_all[(i*B + b)*ss_total + off ...]: ResBlock (scale, shift) for step i, image b.
+  // sin_tab: [nT*B][nf] sinusoidal embeddings (row i*B+b = step i).
+  void tables(Run& r, const float* sin_tab, int nT, const float* tc, const float* icx, int B,
+              float* ss_all, float* cc) {
+    const int R = nT * B;
+    float* h1 = r.alloc<float>((size_t)R * tdim);
+    float* temb = r.alloc<float>((size_t)R * tdim);
+    float* pe = nullptr;
+    if (degra && tc) {
+      float* p0 = r.alloc<float>((size_t)B * tdim);
+      float* p1 = r.alloc<float>((size_t)B * tdim);
+      float* p2 = r.alloc<float>((size_t)B * tdim);
+      pe = r.alloc<float>((size_t)B * tdim);
+      if (!r.dry) {
+        small_linear(tc, ctx, t0w, t0b, p0, tdim, B, ctx, tdim, ACT_NONE, ACT_SILU, nullptr, 0, 1, r.st);
+        small_linear(p0, tdim, t2w, t2b, p1, tdim, B, tdim, tdim, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
+        softmax_mul(p1, prompt, p2, B, tdim, r.st);
+        small_linear(p2, tdim, pmw, pmb, pe, tdim, B, tdim, tdim, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
+      }
+    }
+    if (!r.dry) {
+      small_linear(sin_tab, nf, tm1w, tm1b, h1, tdim, R, nf, tdim, ACT_NONE, ACT_GELU, nullptr, 0, 1, r.st);
+      small_linear(h1, tdim, tm3w, tm3b, temb, tdim, R, tdim, tdim, ACT_NONE, ACT_NONE, pe, tdim, B, r.st);
+    }
+    auto rbt = [&](const RB& rb) {
+      if (!r.dry)
+        small_linear(temb, tdim, rb.mw, rb.mb, ss_all + rb.ss_off, ss_total, R, tdim,
+                     2 * rb.dout, ACT_SILU, ACT_NONE, nullptr, 0, 1, r.st);
+    };
+    for (auto& L : downs) { rbt(L.b1); rbt(L.b2); }
+    for (auto& L : ups) { rbt(L.b1); rbt(L.b2); }
+    rbt(mid1); rbt(mid2); rbt(fin);
+    auto stc = [&](const Attn& a) {
+      if (!a.st) return;
+      const int C = a.s.pin.cout;
+      float* v = r.alloc<float>((size_t)B * C);
+      if (!r.dry) {
+        small_linear(icx, ctx, a.s.a2v, nullptr, v, C, B, ctx, C, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
+        small_linear(v, C, a.s.a2o, a.s.a2ob, cc + a.s.cc_off, cc_total, B, C, C, ACT_NONE,
+                     ACT_NONE, nullptr, 0, 1, r.st);
+      }
+    };
+    for (auto& L : downs) stc(L.at);
+    stc(mid_attn);
+    for (auto& L : ups) stc(L.at);
+  }
+
+  // ----------------------------------------------------------------- blocks
+  const void* resblock(Run& r, const RB& rb, const void* xa, int Ca, const void* xb, int Cb,
+                       int B, int H, int W, const float* ss) {
+    const size_t M = (size_t)B * H * W;
+    T* h1 = r.alloc<T>(M * rb.dout);
+    Epi e1;
+    e1.ss = ss + rb.ss_off; e1.ss_ld = ss_total; e1.act = ACT_SILU;
+    conv_call<T>(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h1, rb.dout, e1);
+    const void* res = xa;
+    int ldr = Ca;
+    if (rb.has_res) {
+      T* rr = r.alloc<T>(M * rb.dout);
+      conv_call<T>(r, rb.res, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 0, rr, rb.dout, Epi());
+      res = rr;
+      ldr = rb.dout;
+    }
+    T* o = r.alloc<T>(M * rb.dout);
+    Epi e2;
+    e2.act = ACT_SILU; e2.res1 = res; e2.ldr1 = ldr;
+    conv_call<T>(r, rb.c2, h1, rb.dout, rb.dout, nullptr, 0, B, H, W, 0, 1, 1, o, rb.dout, e2);
+    return o;
+  }
+
+  const void* linattn(Run& r, const LA& la, const void* x, int C, int B, int H, int W) {
+    const size_t M = (size_t)B * H * W;
+    T* xn = r.alloc<T>(M * C);
+    ln<T>(r, x, C, xn, C, nullptr, 0, la.gpre, nullptr, (int)M, C, 1e-5f);
+    T* qkv = r.alloc<T>(M * 384);
+    conv_call<T>(r, la.qkv, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 384, Epi());
+    T* o = r.alloc<T>(M * 128);
+    float* ws = r.alloc<float>(linear_attention_ws_floats(B, H * W));
+    r.flops += 2.0 * 2.0 * M * 4 * 32 * 32;      // k v^T and ctx^T q (module_util.py:181-183)
+    if (!r.dry) linear_attention<T>(qkv, o, B, H * W, ws, r.st);
+    T* t = r.alloc<T>(M * C);
+    conv_call<T>(r, la.out, o, 128, 128, nullptr, 0, B, H, W, 0, 1, 0, t, C, Epi());
+    T* y = r.alloc<T>(M * C);
+    ln<T>(r, t, C, y, C, x, C, la.gout, nullptr, (int)M, C, 1e-5f);
+    return y;
+  }
+
+  const void* sptrans(Run& r, const ST& s, const void* x, int C, int B, int H, int W,
+                      const float* cc) {
+    const int L = H * W;
+    const size_t M = (size_t)B * L;
+    T* xn = r.alloc<T>(M * C);
+    ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
+    T* gn = r.alloc<T>(M * C);
+    float* stats = r.alloc<float>((size_t)B * 64);
+    if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
+    T* hh = r.alloc<T>(M * C);
+    conv_call<T>(r, s.pin, gn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, Epi());
+    T* a = r.alloc<T>(M * C);
+    ln<T>(r, hh, C, a, C, nullptr, 0, s.n1w, s.n1b, (int)M, C, 1e-5f);
+    T* qkv = r.alloc<T>(M * 3 * C);
+    conv_call<T>(r, s.qkv, a, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 3 * C, Epi());
+    T* o = r.alloc<T>(M * C);
+    r.flops += 4.0 * B * (double)L * L * C;     // QK^T and PV
+    if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, 0.17677669529663687f, r.st);
+    T* h2 = r.alloc<T>(M * C);
+    Epi e;
+    e.res1 = hh; e.ldr1 = C; e.bbias = cc + s.cc_off; e.bb_ld = cc_total;
+    conv_call<T>(r, s.o, o, C, C, nullptr, 0, B, H, W, 0, 1, 0, h2, C, e);
+    T* f = r.alloc<T>(M * C);
+    ln<T>(r, h2, C, f, C, nullptr, 0, s.n3w, s.n3b, (int)M, C, 1e-5f);
+    T* g = r.alloc<T>(M * 4 * C);
+    Epi eg;
+    eg.act = ACT_GEGLU;
+    conv_call<T>(r, s.ff1, f, C, C, nullptr, 0, B, H, W, 0, 1, 0, g, 4 * C, eg);
+    T* h4 = r.alloc<T>(M * C);
+    Epi e4;
+    e4.res1 = h2; e4.ldr1 = C;
+    conv_call<T>(r, s.ff2, g, 4 * C, 4 * C, nullptr, 0, B, H, W, 0, 1, 0, h4, C, e4);
+    T* y = r.alloc<T>(M * C);
+    Epi e5;
+    e5.res1 = xn; e5.ldr1 = C; e5.res2 = x; e5.ldr2 = C;
+    conv_call<T>(r, s.pout, h4, C, C, nullptr, 0, B, H, W, 0, 1, 0, y, C, e5);
+    return y;
+  }
+
+  const void* attn(Run& r, const Attn& a, const void* x, int C, int B, int H, int W,
+                   const float* cc) {
+    return a.st ? sptrans(r, a.s, x, C, B, H, W, cc) : linattn(r, a.la, x, C, B, H, W);
+  }
+
+  int pad_of(int n) const {
+    const int s = 1 << depth;
+    return n + (s - n % s) % s;
+  }
+
+  // One forward. ss: [B][ss_total] of this step; out: [B*Hp*Wp][ldo] (channels < out_nc).
+  void forward(Run& r, const float* xt, const float* mu, int B, int H, int W, const float* ss,
+               const float* cc, void* out, int ldo) {
+    const int Hp = pad_of(H), Wp = pad_of(W);
+    const size_t M0 = (size_t)B * Hp * Wp;
+    T* xin = r.alloc<T>(M0 * 8);
+    if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
+    T* x0 = r.alloc<T>(M0 * nf);
+    conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
+    std::vector<std::pair<const void*, int>> hs;
+    const void* cur = x0;
+    int h = Hp, w = Wp;
+    for (int i = 0; i < depth; ++i) {
+      const auto [din, dout] = levels[i];
+      Level& L = downs[i];
+      cur = resblock(r, L.b1, cur, din, nullptr, 0, B, h, w, ss);
+      hs.push_back({cur, din});
+      cur = resblock(r, L.b2, cur, din, nullptr, 0, B, h, w, ss);
+      cur = attn(r, L.at, cur, din, B, h, w, cc);
+      hs.push_back({cur, din});
+      if (i != depth - 1) {
+        T* y = r.alloc<T>((size_t)B * (h / 2) * (w / 2) * dout);
+        conv_call<T>(r, L.samp, cur, din, din, nullptr, 0, B, h, w, 0, 2, 1, y, dout, Epi());
+        h /= 2; w /= 2;
+        cur = y;
+      } else {
+        T* y = r.alloc<T>((size_t)B * h * w * dout);
+        conv_call<T>(r, L.samp, cur, din, din, nullptr, 0, B, h, w, 0, 1, 1, y, dout, Epi());
+        cur = y;
+      }
+    }
+    const int mid = levels.back().second;
+    cur = resblock(r, mid1, cur, mid, nullptr, 0, B, h, w, ss);
+    cur = attn(r, mid_attn, cur, mid, B, h, w, cc);
+    cur = resblock(r, mid2, cur, mid, nullptr, 0, B, h, w, ss);
+    for (int j = 0; j < depth; ++j) {
+      const int i = depth - 1 - j;
+      const auto [din, dout] = levels[i];
+      Level& L = ups[j];
+      auto sk = hs.back(); hs.pop_back();
+      cur = resblock(r, L.b1, cur, dout, sk.first, sk.second, B, h, w, ss);
+      sk = hs.back(); hs.pop_back();
+      cur = resblock(r, L.b2, cur, dout, sk.first, sk.second, B, h, w, ss);
+      cur = attn(r, L.at, cur, dout, B, h, w, cc);
+      if (i != 0) {
+        T* y = r.alloc<T>((size_t)B * (2 * h) * (2 * w) * din);
+        conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 1, 1, 1, y, din, Epi());
+        h *= 2; w *= 2;
+        cur = y;
+      } else {
+        T* y = r.alloc<T>((size_t)B * h * w * din);
+        conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 0, 1, 1, y, din, Epi());
+        cur = y;
+      }
+    }
+    cur = resblock(r, fin, cur, nf, x0, nf, B, h, w, ss);
+    conv_call<T>(r, final_conv, cur, nf, nf, nullptr, 0, B, h, w, 0, 1, 1, out, ldo, Epi());
+  }
+};
+
+// ============================================================================= ViT
+template <typename T>
+struct VitNet {
+  struct Block { const float *l1w, *l1b, *l2w, *l2b; ConvW qkv, out, fc, proj; };
+  struct Tower { ConvW conv1; const float *cls, *pos, *prew, *preb, *postw, *postb, *projT;
+                 std::vector<Block> blocks; std::vector<ConvW> zero; };
+  dac_config cfg;
+  int S, P, D, layers, heads, hd, mlp, E, G, L;
+  Tower main, ctl;
+  explicit VitNet(const dac_config& c) : cfg(c) {
+    S = c.image_size; P = c.patch_size; D = c.width; layers = c.layers; hd = c.head_width;
+    heads = D / hd; mlp = c.mlp_width; E = c.embed_dim; G = S / P; L = G * G + 1;
+  }
+  Tower load_tower(Packer<T>& Pk, const std::string& p, bool control) {
+    Tower t;
+    t.conv1 = Pk.conv(p + "conv1.weight", D, 3, P, P);
+    t.cls = Pk.f32(p + "class_embedding", {D});
+    t.pos = Pk.f32(p + "positional_embedding", {L, D});
+    t.prew = Pk.f32(p + "ln_pre.weight", {D});
+    t.preb = Pk.f32(p + "ln_pre.bias", {D});
+    t.postw = Pk.f32(p + "ln_post.weight", {D});
+    t.postb = Pk.f32(p + "ln_post.bias", {D});
+    t.projT = Pk.f32_t(p + "proj", D, E);
+    const std::string rb = p + (control ? "transformer.transformer.resblocks." : "transformer.resblocks.");
+    for (int l = 0; l < layers; ++l) {
+      const std::string q = rb + std::to_string(l) + ".";
+      Block b;
+      b.l1w = Pk.f32(q + "ln_1.weight", {D});
+      b.l1b = Pk.f32(q + "ln_1.bias", {D});
+      b.qkv = Pk.linear(q + "attn.in_proj_weight", 3 * D, D, q + "attn.in_proj_bias");
+      b.out = Pk.linear(q + "attn.out_proj.weight", D, D, q + "attn.out_proj.bias");
+      b.l2w = Pk.f32(q + "ln_2.weight", {D});
+      b.l2b = Pk.f32(q + "ln_2.bias", {D});
+      b.fc = Pk.linear(q + "mlp.c_fc.weight", mlp, D, q + "mlp.c_fc.bias");
+      b.proj = Pk.linear(q + "mlp.c_proj.weight", D, mlp, q + "mlp.c_proj.bias");
+      t.blocks.push_back(b);
+      if (control)
+        t.zero.push_back(Pk.linear(p + "transformer.zero_modules." + std::to_string(l) + ".weight",
+                                   D, D, p + "transformer.zero_modules." + std::to_string(l) + ".bias"));
+    }
+    return t;
+  }
+  void load(Packer<T>& Pk, WStore& ws) {
+    // `visual.*` aliases `clip.visual.*` (daclip_model.py:21): accept either spelling.
+    std::vector<std::string> alias;
+    for (auto& kv : ws.m)
+      if (kv.first.rfind("visual.", 0) == 0) alias.push_back(kv.first);
+    for (auto& k : alias) {
+      const std::string c = "clip." + k;
+      if (!ws.m.count(c)) ws.m[c] = ws.m[k];
+      ws.m[k].used = true;
+    }
+    main = load_tower(Pk, "clip.visual.", false);
+    ctl = load_tower(Pk, "visual_control.", true);
+  }
+  void tower(Run& r, const Tower& tw, const void* xin, int B, bool control,
+             std::vector<const void*>* hid_out, const std::vector<const void*>* hid_in,
+             float* out) {
+    constexpr int VE = sizeof(T) == 2 ? 8 : 4;
+    const size_t Mt = (size_t)B * L;
+    T* patch = r.alloc<T>((size_t)B * G * G * D);
+    conv_call<T>(r, tw.conv1, xin, VE, VE, nullptr, 0, B, S, S, 0, P, 0, patch, D, Epi());
+    T* tok = r.alloc<T>(Mt * D);
+    if (!r.dry) vit_embed<T>(patch, tw.cls, tw.pos, tok, B, L, D, r.st);
+    T* x = r.alloc<T>(Mt * D);
+    ln<T>(r, tok, D, x, D, nullptr, 0, tw.prew, tw.preb, (int)Mt, D, 1e-5f);
+    for (int l = 0; l < layers; ++l) {
+      const Block& b = tw.blocks[l];
+      T* a = r.alloc<T>(Mt * D);
+      ln<T>(r, x, D, a, D, nullptr, 0, b.l1w, b.l1b, (int)Mt, D, 1e-5f);
+      T* qkv = r.alloc<T>(Mt * 3 * D);
+      conv_call<T>(r, b.qkv, a, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, qkv, 3 * D, Epi());
+      T* o = r.alloc<T>(Mt * D);
+      r.flops += 4.0 * B * (double)L * L * D;
+      if (!r.dry) small_mha<T>(qkv, o, B, L, heads, hd, r.st);
+      T* x2 = r.alloc<T>(Mt * D);
+      Epi e1;
+      e1.res1 = x; e1.ldr1 = D;
+      conv_call<T>(r, b.out, o, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x2, D, e1);
+      T* a2 = r.alloc<T>(Mt * D);
+      ln<T>(r, x2, D, a2, D, nullptr, 0, b.l2w, b.l2b, (int)Mt, D, 1e-5f);
+      T* f = r.alloc<T>(Mt * mlp);
+      Epi eg;
+      eg.act = ACT_GELU;
+      conv_call<T>(r, b.fc, a2, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, f, mlp, eg);
+      T* x3 = r.alloc<T>(Mt * D);
+      Epi e3;
+      e3.res1 = x2; e3.ldr1 = D;
+      if (hid_in) { e3.res2 = (*hid_in)[layers - 1 - l]; e3.ldr2 = D; }   // control.pop()
+      conv_call<T>(r, b.proj, f, mlp, mlp, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x3, D, e3);
+      if (control) {
+        T* hz = r.alloc<T>(Mt * D);
+        conv_call<T>(r, tw.zero[l], x3, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, hz, D, Epi());
+        hid_out->push_back(hz);
+      }
+      x = x3;
+    }
+    T* pooled = r.alloc<T>((size_t)B * D);
+    ln<T>(r, x, L * D, pooled, D, nullptr, 0, tw.postw, tw.postb, B, D, 1e-5f);
+    float* pf = r.alloc<float>((size_t)B * D);
+    r.flops += 2.0 * B * D * E;
+    if (!r.dry) {
+      rows_to_f32<T>(pooled, D, pf, B, D, r.st);
+      small_linear(pf, D, tw.projT, nullptr, out, E, B, D, E, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
+    }
+  }
+  void encode(Run& r, const float* img, int B, float* ic, float* dc) {
+    constexpr int VE = sizeof(T) == 2 ? 8 : 4;
+    T* xin = r.alloc<T>((size_t)B * S * S * VE);
+    if (!r.dry) vit_prep<T>(img, xin, B, S, r.st);
+    std::vector<const void*> hid;
+    tower(r, ctl, xin, B, true, &hid, nullptr, dc);
+    tower(r, main, xin, B, false, nullptr, &hid, ic);
+  }
+};
+
+// ============================================================================= engine
+template <typename T>
+class EngineT : public Engine {
+ public:
+  EngineT(int device, const dac_config& c) : dev(device), cfg(c) {
+    HIP_OK(hipSetDevice(dev));
+    HIP_OK(hipStreamCreateWithFlags(&priv, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+    if (c.unet) unet = std::make_unique<UNetNet<T>>(c);
+    if (c.vit) {
+      if (c.image_size % c.patch_size || c.width % c.head_width || c.head_width > 64 ||
+          (c.image_size / c.patch_size) * (c.image_size / c.patch_size) + 1 > 64)
+        throw Error(DAC_E_ARG, "unsupported vision config (needs <= 64 tokens, head_width <= 64)");
+      vit = std::make_unique<VitNet<T>>(c);
+    }
+  }
+  ~EngineT() override {
+    clear_graphs();
+    if (arena.base) (void)hipFree(arena.base);
+    for (auto& kv : bufs) free_bufs(kv.second);
+    (void)hipEventDestroy(ev_in);
+    (void)hipEventDestroy(ev_out);
+    (void)hipStreamDestroy(priv);
+  }
+
+  void finalize(WStore& ws) override {
+    HIP_OK(hipSetDevice(dev));
+    Packer<T> P{pool, ws};
+    if (unet) unet->load(P);
+    if (vit) vit->load(P, ws);
+    if (!ws.missing.empty()) {
+      std::string m = "Missing key(s) in state_dict: ";
+      for (size_t i = 0; i < ws.missing.size(); ++i) m += (i ? ", \"" : "\"") + ws.missing[i] + "\"";
+      throw Error(DAC_E_MISSING, m);
+    }
+    ready = true;
+  }
+
+  // ------------------------------------------------------------------ workspace
+  void ensure_arena(size_t bytes) {
+    if (arena.cap >= bytes) return;
+    if (arena.base) HIP_OK(hipFree(arena.base));
+    clear_graphs();
+    arena.base = nullptr;
+    HIP_OK(hipMalloc(&arena.base, bytes));
+    arena.cap = bytes;
+  }
+  struct Bufs {
+    float *xs = nullptr, *mus = nullptr, *tcs = nullptr, *ics = nullptr, *ss = nullptr,
+          *cc = nullptr, *sin = nullptr;
+    void* out = nullptr;
+    uint64_t* seed = nullptr;
+    int ldo = 0;
+  };
+  std::map<std::tuple<int, int, int, int>, Bufs> bufs;    // (B, H, W, nT)
+  void free_bufs(Bufs& b) {
+    for (void* p : {(void*)b.xs, (void*)b.mus, (void*)b.tcs, (void*)b.ics, (void*)b.ss,
+                    (void*)b.cc, (void*)b.sin, b.out, (void*)b.seed})
+      if (p) (void)hipFree(p);
+  }
+  template <class X> X* dalloc(size_t n) {
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, std::max<size_t>(n * sizeof(X), 16)));
+    return (X*)p;
+  }
+  // Sinusoidal time embedding rows [nT*B][nf] for t = times[i] (SinusoidalPosEmb,
+  // module_util.py:41-48, fp32).
+  std::vector<float> sin_table(const std::vector<float>& times, int B) {
+    const int nf = unet->nf, half = nf / 2;
+    const float emb = (float)(std::log(10000.0) / (half - 1));
+    std::vector<float> tab((size_t)times.size() * B * nf);
+    for (size_t i = 0; i < times.size(); ++i)
+      for (int b = 0; b < B; ++b)
+        for (int k = 0; k < half; ++k) {
+          const float f = std::exp((float)k * -emb);
+          const float a = times[i] * f;
+          float* row = tab.data() + (i * B + b) * nf;
+          row[k] = std::sin(a);
+          row[half + k] = std::cos(a);
+        }
+    return tab;
+  }
+  Bufs& get_bufs(int B, int H, int W, int nT) {
+    auto key = std::make_tuple(B, H, W, nT);
+    auto it = bufs.find(key);
+    if (it != bufs.end()) return it->second;
+    Bufs b;
+    const size_t n = (size_t)B * 3 * H * W;
+    const int Hp = unet->pad_of(H), Wp = unet->pad_of(W);
+    b.xs = dalloc<float>(n);
+    b.mus = dalloc<float>(n);
+    b.tcs = dalloc<float>((size_t)B * std::max(1, unet->ctx));
+    b.ics = dalloc<float>((size_t)B * std::max(1, unet->ctx));
+    b.ss = dalloc<float>((size_t)nT * B * unet->ss_total);
+    b.cc = dalloc<float>((size_t)B * std::max(1, unet->cc_total));
+    b.sin = dalloc<float>((size_t)nT * B * unet->nf);
+    b.ldo = 4;
+    b.out = dalloc<char>((size_t)B * Hp * Wp * b.ldo * sizeof(T));
+    b.seed = dalloc<uint64_t>(1);
+    return bufs.emplace(key, b).first->second;
+  }
+  size_t plan_unet(int B, int H, int W, int nT) {
+    Arena a;
+    a.dry = true;
+    Run r;
+    r.dry = true;
+    r.ar = &a;
+    Bufs dummy;
+    unet->tables(r, nullptr, nT, (const float*)1, (const float*)1, B, nullptr, nullptr);
+    const size_t t = a.peak;
+    a.reset();
+    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, nullptr, nullptr, 4);
+    return std::max(t, a.peak) + (1 << 20);
+  }
+  Run live(hipStream_t st) {
+    Run r;
+    r.st = st;
+    r.dry = false;
+    arena.dry = false;
+    r.ar = &arena;
+    return r;
+  }
+
+  // ------------------------------------------------------------------ encode
+  void encode(const float* img, int B, float* ic, float* dc, hipStream_t st) override {
+    need(vit != nullptr, "handle has no vision towers");
+    HIP_OK(hipSetDevice(dev));
+    Arena a;
+    Run d;
+    d.dry = true;
+    d.ar = &a;
+    vit->encode(d, nullptr, B, nullptr, nullptr);
+    ensure_arena(a.peak + (1 << 20));
+    Run r = live(st);
+    arena.reset();
+    vit->encode(r, img, B, ic, dc);
+    HIP_OK(hipGetLastError());
+  }
+
+  // ------------------------------------------------------------------ one UNet call
+  void unet_forward(const float* xt, const float* mu, float t, const float* tc, const float* icx,
+                    int B, int H, int W, float* eps, hipStream_t st) override {
+    need(unet != nullptr, "handle has no UNet");
+    need(!(unet->n_st > 0 && icx == nullptr), "image_context is required (SpatialTransformer)");
+    HIP_OK(hipSetDevice(dev));
+    ensure_arena(plan_unet(B, H, W, 1));
+    Bufs& b = get_bufs(B, H, W, 1);
+    auto tab = sin_table({t}, B);
+    HIP_OK(hipMemcpyAsync(b.sin, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, st));
+    Run r = live(st);
+    arena.reset();
+    unet->tables(r, b.sin, 1, tc, icx, B, b.ss, b.cc);
+    arena.reset();
+    unet->forward(r, xt, mu, B, H, W, b.ss, b.cc, b.out, b.ldo);
+    unet_out<T>(b.out, b.ldo, eps, B, H, W, unet->pad_of(H), unet->pad_of(W), st);
+    HIP_OK(hipGetLastError());
+  }
+
+  void posterior_step(int mode, float* x, const float* eps, const float* mu, const float* z, int t,
+                      int n, hipStream_t st) override {
+    need(sched.T > 0, "schedule not set");
+    need(t >= 1 && t <= sched.T, "t out of range");
+    need(z != nullptr, "posterior_step needs explicit noise");
+    // eps is NCHW here (ld = 0 selects flat indexing in the kernel).
+    sde_step<float>(mode, x, mu, eps, 0, 1, 1, z, nullptr, 0, sched.coef(t, mode), 1, 1, n, st);
+    HIP_OK(hipGetLastError());
+  }
+
+  // ------------------------------------------------------------------ full loop
+  struct GKey {
+    int mode, B, H, W, nT;
+    const float* noise;
+    bool operator<(const GKey& o) const {
+      return std::tie(mode, B, H, W, nT, noise) < std::tie(o.mode, o.B, o.H, o.W, o.nT, o.noise);
+    }
+  };
+  std::map<GKey, hipGraphExec_t> graphs;
+  int graph_prof_id = -1;
+  void clear_graphs() {
+    for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
+  void record_loop(Run& r, Bufs& b, int mode, int B, int H, int W, int nT, const float* noise) {
+    const int Hp = unet->pad_of(H), Wp = unet->pad_of(W);
+    r.ar->reset();
+    unet->tables(r, b.sin, nT, b.tcs, b.ics, B, b.ss, b.cc);
+    const size_t n = (size_t)B * 3 * H * W;
+    for (int i = 0; i < nT; ++i) {
+      const int t = nT - i;
+      r.ar->reset();
+      unet->forward(r, b.xs, b.mus, B, H, W, b.ss + (size_t)i * B * unet->ss_total, b.cc, b.out, b.ldo);
+      if (!r.dry)
+        sde_step<T>(mode, b.xs, b.mus, b.out, b.ldo, Hp, Wp, noise ? noise + (size_t)i * n : nullptr,
+                    b.seed, (uint32_t)t, sched.coef(t, mode), B, H, W, r.st);
+    }
+  }
+  void sde_reverse(int mode, float* x, const float* mu, const float* tc, const float* icx, int B,
+                   int H, int W, int nT, const float* noise, uint64_t seed, hipStream_t st) override {
+    need(unet != nullptr, "handle has no UNet");
+    need(sched.T > 0, "call dac_sde_schedule first");
+    need(nT >= 1 && nT <= sched.T, "T exceeds the schedule length");
+    need(!(unet->n_st > 0 && icx == nullptr), "image_context is required (SpatialTransformer)");
+    HIP_OK(hipSetDevice(dev));
+    ensure_arena(plan_unet(B, H, W, nT));
+    Bufs& b = get_bufs(B, H, W, nT);
+    const size_t n = (size_t)B * 3 * H * W;
+    HIP_OK(hipEventRecord(ev_in, st));
+    HIP_OK(hipStreamWaitEvent(priv, ev_in, 0));
+    HIP_OK(hipMemcpyAsync(b.xs, x, n * 4, hipMemcpyDeviceToDevice, priv));
+    HIP_OK(hipMemcpyAsync(b.mus, mu, n * 4, hipMemcpyDeviceToDevice, priv));
+    if (tc) HIP_OK(hipMemcpyAsync(b.tcs, tc, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
+    if (icx) HIP_OK(hipMemcpyAsync(b.ics, icx, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
+    seed_host = seed;
+    HIP_OK(hipMemcpyAsync(b.seed, &seed_host, 8, hipMemcpyHostToDevice, priv));
+    std::vector<float> times;
+    for (int i = 0; i < nT; ++i) times.push_back((float)(nT - i));
+    auto tab = sin_table(times, B);
+    HIP_OK(hipMemcpyAsync(b.sin, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, priv));
+    HIP_OK(hipStreamSynchronize(priv));       // host staging buffers above are pageable
+    // tc == nullptr is a different program (no prompt embedding): key it via mode bit.
+    const int mkey = mode | (tc ? 0 : 2);
+    GKey key{mkey, B, H, W, nT, noise};
+    if (prof.kernel_id != graph_prof_id) { clear_graphs(); graph_prof_id = prof.kernel_id; }
+    auto it = graphs.find(key);
+    if (it == graphs.end()) {
+      if (prof.kernel_id >= 0) {                 // pre-create the event pairs (count via dry run)
+        Arena da;
+        Run d;
+        d.dry = true;
+        d.ar = &da;
+        d.prof = &prof;
+        prof.begin_pass();
+        record_loop(d, b, mode, B, H, W, nT, noise);
+        while (prof.ev.size() < 2 * prof.used) {
+          hipEvent_t ev;
+          HIP_OK(hipEventCreate(&ev));
+          prof.ev.push_back(ev);
+        }
+      }
+      Run r = live(priv);
+      r.prof = prof.kernel_id >= 0 ? &prof : nullptr;
+      prof.begin_pass();
+      hipGraph_t g;
+      HIP_OK(hipStreamBeginCapture(priv, hipStreamCaptureModeThreadLocal));
+      try {
+        record_loop(r, b, mode, B, H, W, nT, noise);
+      } catch (...) {
+        hipGraph_t dead;
+        (void)hipStreamEndCapture(priv, &dead);
+        if (dead) (void)hipGraphDestroy(dead);
+        throw;
+      }
+      HIP_OK(hipStreamEndCapture(priv, &g));
+      hipGraphExec_t ex;
+      HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      HIP_OK(hipGraphDestroy(g));
+      it = graphs.emplace(key, ex).first;
+    }
+    HIP_OK(hipGraphLaunch(it->second, priv));
+    HIP_OK(hipMemcpyAsync(x, b.xs, n * 4, hipMemcpyDeviceToDevice, priv));
+    HIP_OK(hipEventRecord(ev_out, priv));
+    HIP_OK(hipStreamWaitEvent(st, ev_out, 0));
+  }
+
+  double unet_flops(int B, int H, int W) override {
+    Arena a;
+    Run r;
+    r.dry = true;
+    r.ar = &a;
+    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, nullptr, nullptr, 4);
+    return r.flops;
+  }
+  double encode_flops(int B) override {
+    Arena a;
+    Run r;
+    r.dry = true;
+    r.ar = &a;
+    vit->encode(r, nullptr, B, nullptr, nullptr);
+    return r.flops;
+  }
+
+  static void need(bool c, const char* m) {
+    if (!c) throw Error(DAC_E_ARG, m);
+  }
+
+  int dev;
+  dac_config cfg;
+  bool ready = false;
+  DevPool pool;
+  std::unique_ptr<UNetNet<T>> unet;
+  std::unique_ptr<VitNet<T>> vit;
+  Arena arena;
+  hipStream_t priv;
+  hipEvent_t ev_in, ev_out;
+  uint64_t seed_host = 0;
+};
+
+std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {
+  if (dtype == DAC_F32) return std::make_unique<EngineT<float>>(device, cfg);
+  if (dtype == DAC_BF16) return std::make_unique<EngineT<bf16>>(device, cfg);
+  throw Error(DAC_E_ARG, "dtype must be DAC_F32 or DAC_BF16");
+}
+
+template void conv_call<float>(Run&, const ConvW&, const void*, int, int, const void*, int, int,
+                               int, int, int, int, int, void*, int, const Epi&);
+template void conv_call<bf16>(Run&, const ConvW&, const void*, int, int, const void*, int, int,
+                              int, int, int, int, int, void*, int, const Epi&);
+
+}  // namespace dac

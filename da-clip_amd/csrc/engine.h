@@ -1,0 +1,145 @@
+// engine.h — host-side runtime of libdaclip_hip: weight store + repacking, workspace arena,
+// and the network executors (ConditionalUNet, DaCLIP vision towers, IR-SDE loop).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/daclip_hip.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace dac {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_OK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      throw ::dac::Error(DAC_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+// ----------------------------------------------------------------------------- weights
+struct HostW {
+  std::vector<float> v;
+  std::vector<int64_t> shape;
+  bool used = false;
+};
+
+struct WStore {
+  std::unordered_map<std::string, HostW> m;
+  std::vector<std::string> missing;
+  // Fetch a tensor by reference key; records a miss (strict-load semantics) on absence and
+  // throws on a shape mismatch (torch load_state_dict's size-mismatch error).
+  const HostW* get(const std::string& key, std::vector<int64_t> shape);
+};
+
+// Owns device allocations for packed weights.
+struct DevPool {
+  std::vector<void*> ptrs;
+  ~DevPool();
+  void* alloc(size_t bytes);
+  void* upload(const void* host, size_t bytes);
+};
+
+uint16_t f2bf_host(float f);
+
+// Packed conv/linear weight: [cout][kh][kw][cin] in the compute dtype (+ fp32 bias).
+struct ConvW {
+  const void* w = nullptr;
+  const float* b = nullptr;
+  int cout = 0, cin = 0, cin_real = 0, kh = 1, kw = 1;
+};
+
+// ----------------------------------------------------------------------------- run context
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, off = 0, peak = 0;
+  bool dry = true;
+  void reset() { off = 0; }
+  void* get(size_t bytes) {
+    size_t o = (off + 255) & ~size_t(255);
+    off = o + bytes;
+    if (off > peak) peak = off;
+    if (dry) return reinterpret_cast<void*>(uintptr_t(0x100000) + o);
+    if (off > cap) throw Error(DAC_E_NOMEM, "workspace arena overflow");
+    return base + o;
+  }
+};
+
+struct Profiler {
+  int kernel_id = -1;            // conv class to time (kh*100 + tile), -1 = off
+  std::vector<hipEvent_t> ev;    // start/stop pairs
+  size_t used = 0;               // pairs recorded in the current pass
+  double flops = 0, bytes = 0;   // algorithmic work of the recorded launches
+  size_t launches = 0;
+  void begin_pass() { used = 0; flops = 0; bytes = 0; launches = 0; }
+  ~Profiler();
+};
+
+struct Run {
+  hipStream_t st = nullptr;
+  bool dry = false;
+  Arena* ar = nullptr;
+  Profiler* prof = nullptr;
+  double flops = 0;              // executed FLOPs (2*MAC) accumulated by the launches
+  template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
+};
+
+// Epilogue options for conv_call.
+struct Epi {
+  const float* ss = nullptr; int ss_ld = 0;
+  const void* res1 = nullptr; int ldr1 = 0;
+  const void* res2 = nullptr; int ldr2 = 0;
+  const float* bbias = nullptr; int bb_ld = 0;
+  int act = ACT_NONE;
+};
+
+int conv_tile_id(int cout, int act);
+
+template <typename T>
+void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,
+               int B, int Hs, int Ws, int up, int stride, int pad, void* y, int ldy,
+               const Epi& e);
+
+// ----------------------------------------------------------------------------- networks
+struct SdeSchedule {
+  int T = 0;
+  std::vector<float> thetas, sigmas, tcum, sbar;
+  float dt = 0, max_sigma = 0;
+  StepCoef coef(int t, int mode) const;
+};
+void compute_schedule(SdeSchedule& s, float max_sigma, int T, int schedule, float eps);
+
+class Engine {
+ public:
+  virtual ~Engine() = default;
+  virtual void finalize(WStore& w) = 0;
+  virtual void encode(const float* img, int B, float* ic, float* dc, hipStream_t st) = 0;
+  virtual void unet_forward(const float* xt, const float* mu, float t, const float* tc,
+                            const float* icx, int B, int H, int W, float* eps,
+                            hipStream_t st) = 0;
+  virtual void sde_reverse(int mode, float* x, const float* mu, const float* tc,
+                           const float* icx, int B, int H, int W, int T, const float* noise,
+                           uint64_t seed, hipStream_t st) = 0;
+  virtual void posterior_step(int mode, float* x, const float* eps, const float* mu,
+                              const float* z, int t, int n, hipStream_t st) = 0;
+  virtual double unet_flops(int B, int H, int W) = 0;
+  virtual double encode_flops(int B) = 0;
+  SdeSchedule sched;
+  Profiler prof;
+};
+
+std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg);
+
+}  // namespace dac

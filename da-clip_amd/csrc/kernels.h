@@ -1,0 +1,103 @@
+// kernels.h — host-side launchers of the gfx950 kernels (one .hip file per family).
+// All activations are NHWC ("rows" = pixels/tokens, row stride `ld` elements), stored as
+// T = float (parity mode) or bf16 (perf mode); small per-image vectors are fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dac {
+
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_GEGLU = 3 };
+
+// Implicit-GEMM convolution / linear layer:
+//   y[m, n] = epi( sum_k A[m, k] * W[n, k] ),  m = (b, oh, ow), k = (kh, kw, ci)
+// A gathers the (optionally 2x nearest-upsampled) input; channels [0, C1) come from x1 and
+// [C1, Cin) from x2 (fused torch.cat, DenoisingUNet_arch.py:158-161). W is [Cout][KH][KW][Cin].
+// Epilogue order (module_util.py:121-129, 143-153): +bias -> *(1+scale)+shift (per image) ->
+// act -> +res1 -> +res2 -> +bbias (per image, per channel).
+struct ConvArgs {
+  const void* x1; const void* x2;
+  int ld1, ld2, C1, Cin;
+  int Hs, Ws, up;          // source spatial size; up=1: nearest 2x before the conv
+  int B, Ho, Wo, Cout, K;
+  const void* w;
+  const float* bias;       // [Cout] or null
+  const float* ss;         // scale [b*ss_ld + n], shift [b*ss_ld + Cout + n]; or null
+  int ss_ld;
+  const void* res1; int ldr1;
+  const void* res2; int ldr2;
+  const float* bbias; int bb_ld;   // per-image bias [b*bb_ld + n]; or null
+  void* y; int ldy;
+  int act;
+};
+
+template <typename T>
+void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
+
+// Row LayerNorm over C (channel LN of NHWC == token LN):
+//   y = [res +] (x - mean) * rsqrt(var + eps) * g [+ b]
+template <typename T>
+void layernorm(const void* x, int ldx, void* y, int ldy, const void* res, int ldr,
+               const float* g, const float* b, int rows, int C, float eps, hipStream_t st);
+
+// GroupNorm(groups, eps, affine) on NHWC [B, HW, C] -> y (same layout).
+template <typename T>
+void groupnorm(const void* x, void* y, const float* g, const float* b, int B, int HW, int C,
+               int groups, float eps, float* stats_ws, hipStream_t st);
+
+// Multi-head self-attention over rows of qkv [B*L, 3*H*D] (q | k | v), D = 32 (UNet
+// SpatialTransformer, attention.py:170-193) -> o [B*L, H*D].
+template <typename T>
+void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st);
+
+// nn.MultiheadAttention core for the ViT (L <= 64 tokens, D = 64 or 32).
+template <typename T>
+void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t st);
+
+// LinearAttention (module_util.py:170-185) on qkv [B*HW, 384]:
+//   kernel 1: per (image, pixel chunk) partial k-softmax stats and k v^T context
+//   kernel 2: combine chunks -> ctx[b][h][d][e]  (already / sum_k and / HW)
+//   kernel 3: out[n, h*32+e] = scale * sum_d ctx[d][e] * softmax_d(q)[d]
+template <typename T>
+void linear_attention(const void* qkv, void* out, int B, int HW, float* ws, hipStream_t st);
+size_t linear_attention_ws_floats(int B, int HW);
+
+// Small fp32 dense layer for per-image vectors (time / prompt MLPs, ViT head):
+//   y[r, o] = post( b[o] + sum_i pre(x[r*ldx + i]) * W[o*I + i] ) (+ add[r % add_mod, o])
+void small_linear(const float* x, int ldx, const float* W, const float* b, float* y, int ldy,
+                  int R, int I, int O, int pre_act, int post_act, const float* add, int add_ld,
+                  int add_mod, hipStream_t st);
+// y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)
+void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st);
+
+// UNet input: x[b, h, w, 0:8] = (xt - mu, mu, 0, 0) with reflect padding to (Hp, Wp)
+// (DenoisingUNet_arch.py:123-127). xt, mu: NCHW fp32 [B, 3, H, W].
+template <typename T>
+void unet_prep(const float* xt, const float* mu, void* x, int B, int H, int W, int Hp, int Wp,
+               hipStream_t st);
+
+// Crop the padded NHWC model output (channels [0,3) of rows of stride ld) to NCHW fp32.
+template <typename T>
+void unet_out(const void* y, int ld, float* eps, int B, int H, int W, int Hp, int Wp,
+              hipStream_t st);
+
+// Sampler updates on NCHW fp32 state (sde_utils.py:205-231, 245-247 / 44-45, 177-187).
+// eps is the padded NHWC model output. z: explicit noise or null -> Philox(*seedp, tag).
+struct StepCoef { float sbar, ea, t1, t2, std, theta, sigma2, dt, sigma_sqrt_dt; };
+template <typename T>
+void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
+              const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
+              int W, hipStream_t st);
+
+// ViT input: NCHW fp32 image -> NHWC T with channels padded to VE.
+template <typename T>
+void vit_prep(const float* img, void* x, int B, int S, hipStream_t st);
+// tokens[b, 0] = cls + pos[0]; tokens[b, 1+p] = patch[b, p] + pos[1+p]
+template <typename T>
+void vit_embed(const void* patch, const float* cls, const float* pos, void* tok, int B, int L,
+               int D, hipStream_t st);
+// Gather row 0 of each image's tokens to fp32 [B, D] (after ln_post).
+template <typename T>
+void rows_to_f32(const void* x, int ld, float* y, int R, int D, hipStream_t st);
+
+}  // namespace dac

@@ -1,0 +1,268 @@
+// misc.hip — small kernels around the two networks:
+//  * small_linear / softmax_mul : fp32 per-image MLPs (time_mlp, text_mlp, prompt_mlp,
+//    ResBlock.mlp, cross-attention value path, ViT head), DenoisingUNet_arch.py:51-63,
+//    132-137; module_util.py:135-137, 143-148; transformer.py:546-547.
+//  * unet_prep / unet_out : input concat + reflect pad, output crop (DenoisingUNet_arch.py:
+//    123-127, 172).
+//  * sde_step : IR-SDE posterior / reverse-SDE update with injected or Philox noise
+//    (sde_utils.py:44-45, 177-187, 205-231, 245-247).
+//  * vit_prep / vit_embed / rows_to_f32 : ViT stem and pooled-token extraction
+//    (transformer.py:518-532, 543-544).
+#include "common.h"
+#include "kernels.h"
+
+namespace dac {
+
+__device__ __forceinline__ float act_f(float v, int a) {
+  return a == ACT_SILU ? silu_f(v) : a == ACT_GELU ? gelu_f(v) : v;
+}
+
+// One wave per output element group; lanes split the reduction (coalesced W rows).
+__global__ void __launch_bounds__(256) small_linear_kernel(const float* __restrict__ x, int ldx,
+                                                           const float* __restrict__ W,
+                                                           const float* b, float* y, int ldy,
+                                                           int R, int I, int O, int pre,
+                                                           int post, const float* add,
+                                                           int add_ld, int add_mod) {
+  extern __shared__ float xs[];
+  const int r = blockIdx.y;
+  for (int i = threadIdx.x; i < I; i += 256) xs[i] = act_f(x[(size_t)r * ldx + i], pre);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int o0 = blockIdx.x * 32 + wave * 8;
+  for (int oi = 0; oi < 8; ++oi) {
+    const int o = o0 + oi;
+    if (o >= O) break;
+    float s = 0.f;
+    for (int i = lane; i < I; i += 64) s += xs[i] * W[(size_t)o * I + i];
+    s = wave_sum(s);
+    if (lane == 0) {
+      float v = s + (b ? b[o] : 0.f);
+      v = act_f(v, post);
+      if (add) v += add[(size_t)(r % add_mod) * add_ld + o];
+      y[(size_t)r * ldy + o] = v;
+    }
+  }
+}
+
+void small_linear(const float* x, int ldx, const float* W, const float* b, float* y, int ldy,
+                  int R, int I, int O, int pre, int post, const float* add, int add_ld,
+                  int add_mod, hipStream_t st) {
+  dim3 g((O + 31) / 32, R);
+  small_linear_kernel<<<g, 256, I * sizeof(float), st>>>(x, ldx, W, b, y, ldy, R, I, O, pre,
+                                                          post, add, add_ld, add_mod > 0 ? add_mod : 1);
+}
+
+__global__ void __launch_bounds__(256) softmax_mul_kernel(const float* x, const float* v,
+                                                          float* y, int C) {
+  const int r = blockIdx.x;
+  __shared__ float red[4];
+  __shared__ float bc;
+  const float* xr = x + (size_t)r * C;
+  float m = -INFINITY;
+  for (int i = threadIdx.x; i < C; i += 256) m = fmaxf(m, xr[i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) bc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  m = bc;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < C; i += 256) s += expf(xr[i] - m);
+  s = wave_sum(s);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bc = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += 256) y[(size_t)r * C + i] = expf(xr[i] - m) / bc * v[i];
+}
+
+void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st) {
+  softmax_mul_kernel<<<R, 256, 0, st>>>(x, v, y, C);
+}
+
+// --------------------------------------------------------------------------- UNet I/O
+template <typename T>
+__global__ void unet_prep_kernel(const float* xt, const float* mu, T* x, int B, int H, int W,
+                                 int Hp, int Wp) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t n = (size_t)B * Hp * Wp;
+  if (i >= n) return;
+  const int w = (int)(i % Wp);
+  const int h = (int)((i / Wp) % Hp);
+  const int b = (int)(i / ((size_t)Wp * Hp));
+  const int sh = h < H ? h : 2 * (H - 1) - h;     // F.pad(..., 'reflect')
+  const int sw = w < W ? w : 2 * (W - 1) - w;
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const size_t o = (((size_t)b * 3 + c) * H + sh) * W + sw;
+    const float m = mu[o];
+    v[c] = xt[o] - m;
+    v[3 + c] = m;
+  }
+  v[6] = v[7] = 0.f;
+  T* dst = x + i * 8;
+  if constexpr (sizeof(T) == 2) {
+    store_vec<T>(dst, v);
+  } else {
+    store_vec<T>(dst, v);
+    store_vec<T>(dst + 4, v + 4);
+  }
+}
+
+template <typename T>
+void unet_prep(const float* xt, const float* mu, void* x, int B, int H, int W, int Hp, int Wp,
+               hipStream_t st) {
+  const size_t n = (size_t)B * Hp * Wp;
+  unet_prep_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(xt, mu, (T*)x, B, H, W, Hp, Wp);
+}
+
+template <typename T>
+__global__ void unet_out_kernel(const T* y, int ld, float* eps, int B, int H, int W, int Hp,
+                                int Wp) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t n = (size_t)B * 3 * H * W;
+  if (i >= n) return;
+  const int w = (int)(i % W);
+  const int h = (int)((i / W) % H);
+  const int c = (int)((i / ((size_t)W * H)) % 3);
+  const int b = (int)(i / ((size_t)W * H * 3));
+  eps[i] = to_f(y[(((size_t)b * Hp + h) * Wp + w) * ld + c]);
+}
+
+template <typename T>
+void unet_out(const void* y, int ld, float* eps, int B, int H, int W, int Hp, int Wp,
+              hipStream_t st) {
+  const size_t n = (size_t)B * 3 * H * W;
+  unet_out_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const T*)y, ld, eps, B, H, W,
+                                                                  Hp, Wp);
+}
+
+// --------------------------------------------------------------------------- sampler
+// Philox4x32-10 counter-based generator (Salmon et al., SC'11), Box-Muller to N(0,1).
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t tag, uint64_t i) {
+  const uint4 r = philox(make_uint4((uint32_t)(i >> 1), (uint32_t)(i >> 33), tag, 0x5DAC11Fu),
+                         make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  const float u1 = ((i & 1 ? r.z : r.x) >> 8) * (1.f / 16777216.f) + (0.5f / 16777216.f);
+  const float u2 = ((i & 1 ? r.w : r.y) >> 8) * (1.f / 16777216.f);
+  return sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+}
+
+template <typename T>
+__global__ void sde_step_kernel(int mode, float* x, const float* mu, const T* eps, int ld, int Hp,
+                                int Wp, const float* z, const uint64_t* seedp, uint32_t tag,
+                                StepCoef c, int H, int W, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int w = (int)(i % W);
+  const int h = (int)((i / W) % H);
+  const int ch = (int)((i / ((size_t)W * H)) % 3);
+  const int b = (int)(i / ((size_t)W * H * 3));
+  const float e = ld == 0 ? to_f(eps[i]) : to_f(eps[(((size_t)b * Hp + h) * Wp + w) * ld + ch]);
+  const float xv = x[i], m = mu[i];
+  const float zv = z ? z[i] : philox_normal(*seedp, tag, i);
+  float out;
+  if (mode == 0) {
+    const float x0 = ((xv - m) - c.sbar * e) * c.ea + m;                  // sde_utils.py:245-247
+    const float mean = c.t1 * (xv - m) + c.t2 * (x0 - m) + m;             // :205-213
+    out = mean + c.std * zv;                                              // :227-231
+  } else {
+    const float score = -e / c.sbar;                                      // :186-187
+    const float drift = (c.theta * (m - xv) - c.sigma2 * score) * c.dt;   // :177-178
+    out = xv - drift - c.sigma_sqrt_dt * zv;                              // :44-45, 183-184
+  }
+  x[i] = out;
+}
+
+template <typename T>
+void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
+              const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
+              int W, hipStream_t st) {
+  const size_t n = (size_t)B * 3 * H * W;
+  sde_step_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld,
+                                                                  Hp, Wp, z, seedp, tag, c, H, W, n);
+}
+
+// --------------------------------------------------------------------------- ViT stem
+template <typename T>
+__global__ void vit_prep_kernel(const float* img, T* x, int B, int S) {
+  constexpr int VE = TypeInfo<T>::VE;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t n = (size_t)B * S * S;
+  if (i >= n) return;
+  const int w = (int)(i % S), h = (int)((i / S) % S), b = (int)(i / ((size_t)S * S));
+  float v[VE];
+#pragma unroll
+  for (int c = 0; c < VE; ++c) v[c] = c < 3 ? img[(((size_t)b * 3 + c) * S + h) * S + w] : 0.f;
+  store_vec<T>(x + i * VE, v);
+}
+
+template <typename T>
+void vit_prep(const float* img, void* x, int B, int S, hipStream_t st) {
+  const size_t n = (size_t)B * S * S;
+  vit_prep_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(img, (T*)x, B, S);
+}
+
+template <typename T>
+__global__ void vit_embed_kernel(const T* patch, const float* cls, const float* pos, T* tok,
+                                 int L, int D, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int d = (int)(i % D);
+  const int t = (int)((i / D) % L);
+  const int b = (int)(i / ((size_t)D * L));
+  const float v = t == 0 ? cls[d] : to_f(patch[((size_t)b * (L - 1) + t - 1) * D + d]);
+  tok[i] = from_f<T>(v + pos[(size_t)t * D + d]);
+}
+
+template <typename T>
+void vit_embed(const void* patch, const float* cls, const float* pos, void* tok, int B, int L,
+               int D, hipStream_t st) {
+  const size_t n = (size_t)B * L * D;
+  vit_embed_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const T*)patch, cls, pos,
+                                                                   (T*)tok, L, D, n);
+}
+
+template <typename T>
+__global__ void rows_to_f32_kernel(const T* x, int ld, float* y, int D, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  y[i] = to_f(x[(i / D) * ld + i % D]);
+}
+
+template <typename T>
+void rows_to_f32(const void* x, int ld, float* y, int R, int D, hipStream_t st) {
+  const size_t n = (size_t)R * D;
+  rows_to_f32_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const T*)x, ld, y, D, n);
+}
+
+#define INST(T)                                                                               \
+  template void unet_prep<T>(const float*, const float*, void*, int, int, int, int, int,      \
+                             hipStream_t);                                                    \
+  template void unet_out<T>(const void*, int, float*, int, int, int, int, int, hipStream_t);  \
+  template void sde_step<T>(int, float*, const float*, const void*, int, int, int,            \
+                            const float*, const uint64_t*, uint32_t, StepCoef, int, int, int, \
+                            hipStream_t);                                                     \
+  template void vit_prep<T>(const float*, void*, int, int, hipStream_t);                      \
+  template void vit_embed<T>(const void*, const float*, const float*, void*, int, int, int,   \
+                             hipStream_t);                                                    \
+  template void rows_to_f32<T>(const void*, int, float*, int, int, hipStream_t);
+INST(float)
+INST(bf16)
+#undef INST
+
+}  // namespace dac

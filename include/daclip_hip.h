@@ -1,0 +1,129 @@
+/*
+ * daclip_hip.h — C ABI of libdaclip_hip.so, the MI355X-native DA-CLIP + IR-SDE hot path.
+ *
+ * The reference (yeeecheng/DA-CLIP) has no native plugin API; its plug points are Python
+ * callables. Each entry point below replaces one of them:
+ *
+ *   dac_create / dac_set_weight / dac_finalize_weights
+ *       replace module construction + strict `load_state_dict`:
+ *       open_clip/factory.py:99-106 (load_checkpoint), factory.py:365-404
+ *       (create_model_from_pretrained), config/daclip-sde/models/base_model.py:92-105
+ *       (load_network) and networks.py:10-15 (define_G -> ConditionalUNet(**setting)).
+ *   dac_encode_image
+ *       replaces DaCLIP.encode_image(image, control=True)   (open_clip/daclip_model.py:46-53)
+ *   dac_unet_forward
+ *       replaces the `sde.set_model(model)` callable: model(x, mu, t, text_context=,
+ *       image_context=) -> noise (utils/sde_utils.py:163-164, 195-202;
+ *       DenoisingUNet_arch.py:118-174)
+ *   dac_sde_schedule
+ *       replaces IRSDE._initialize                          (utils/sde_utils.py:84-154)
+ *   dac_sde_reverse
+ *       replaces IRSDE.reverse_posterior / reverse_sde      (utils/sde_utils.py:261-313)
+ *       as one hipGraph-captured loop
+ *   dac_posterior_step
+ *       replaces IRSDE.reverse_posterior_step / reverse_sde_step (sde_utils.py:44-45, 227-231)
+ *
+ * Conventions: every tensor argument is a caller-owned DEVICE pointer to contiguous fp32
+ * NCHW data (torch `data_ptr()`), on the handle's device. `stream` is a hipStream_t (NULL =
+ * default stream). Functions return 0 on success and a negative DAC_E* code on error; the
+ * message is available from dac_last_error(). A handle owns its weights, workspace and
+ * graphs; calls on one handle must be serialised; handles on different devices are
+ * independent (one handle per GPU / rank).
+ */
+#ifndef DACLIP_HIP_H
+#define DACLIP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dac_handle dac_handle;
+
+enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1 };           /* compute/storage dtype */
+enum dac_src_dtype { DAC_SRC_F32 = 0, DAC_SRC_F16 = 1, DAC_SRC_BF16 = 2 };
+enum dac_mode { DAC_POSTERIOR = 0, DAC_SDE = 1 };       /* DenoisingModel.test(mode=) */
+enum dac_schedule { DAC_COSINE = 0, DAC_LINEAR = 1, DAC_CONSTANT = 2 };
+
+enum dac_err {
+  DAC_OK = 0,
+  DAC_E_ARG = -1,        /* bad argument / shape / dtype */
+  DAC_E_KEY = -2,        /* unknown state_dict key or shape mismatch */
+  DAC_E_MISSING = -3,    /* dac_finalize_weights: required key never set (strict load) */
+  DAC_E_STATE = -4,      /* call order (e.g. forward before finalize) */
+  DAC_E_HIP = -5,        /* HIP runtime error */
+  DAC_E_NOMEM = -6
+};
+
+/* Network configuration. UNet fields mirror options/test.yml network_G.setting
+ * (DenoisingUNet_arch.py:22-23); vision fields mirror CLIPVisionCfg
+ * (open_clip/model_configs/daclip_ViT-B-32.json). Zero `unet`/`vit` skips that network. */
+typedef struct dac_config {
+  int unet;
+  int in_nc, out_nc, nf, depth, ch_mult[8], context_dim;
+  int use_degra_context, use_image_context;
+  int vit;
+  int image_size, patch_size, width, layers, head_width, mlp_width, embed_dim;
+} dac_config;
+
+int dac_create(int device, int dtype, const dac_config* cfg, dac_handle** out);
+void dac_destroy(dac_handle* h);
+
+/* Copy one reference state_dict tensor (host or device pointer) into the handle,
+ * repacking it to the kernel layout. Keys use the reference names, e.g.
+ * "downs.0.0.block1.proj.weight", "clip.visual.transformer.resblocks.0.attn.in_proj_weight",
+ * "visual_control.transformer.zero_modules.0.weight". Keys the hot path does not use
+ * (text tower, logit_scale) are accepted and ignored (returns 1). */
+int dac_set_weight(dac_handle* h, const char* key, const void* data, const int64_t* shape,
+                   int ndim, int src_dtype);
+/* Strict check: every key the configured networks need was set. */
+int dac_finalize_weights(dac_handle* h);
+
+/* img [B,3,S,S] (preprocessed, S = image_size) -> image_ctx [B,E], degra_ctx [B,E] fp32. */
+int dac_encode_image(dac_handle* h, const float* img, int B, float* image_ctx,
+                     float* degra_ctx, void* stream);
+
+/* One ConditionalUNet forward: eps = model(xt, mu, t, text_ctx, image_ctx), all [B,3,H,W]
+ * except contexts [B,context_dim]; text_ctx / image_ctx may be NULL. */
+int dac_unet_forward(dac_handle* h, const float* xt, const float* mu, float t,
+                     const float* text_ctx, const float* image_ctx, int B, int H, int W,
+                     float* eps_out, void* stream);
+
+/* IR-SDE schedule. If `tables` is non-NULL it holds 4*(T+1) host floats
+ * [thetas | sigmas | thetas_cumsum | sigma_bars] computed by the caller (bit-identical to the
+ * reference's torch ops) and `dt` is used as given; otherwise the tables are computed here
+ * in fp32 following sde_utils.py:91-154. */
+int dac_sde_schedule(dac_handle* h, float max_sigma, int T, int schedule, float eps,
+                     const float* tables, float dt);
+
+/* Full reverse loop t = T..1 in place on x_inout [B,3,H,W] with mu = LQ [B,3,H,W].
+ * noise: NULL -> device Philox N(0,1) keyed by (seed, step, element); else [T,B,3,H,W]
+ * fp32 device tensor, slice i consumed at step t = T - i (parity mode). Captured once per
+ * (B,H,W,T,mode) as a hipGraph and replayed. */
+int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu,
+                    const float* text_ctx, const float* image_ctx, int B, int H, int W, int T,
+                    const float* noise, uint64_t seed, void* stream);
+
+/* One sampler update given the model output: x <- step(x, eps, t, z) (z: [B,3,H,W]). */
+int dac_posterior_step(dac_handle* h, int mode, float* x_inout, const float* eps,
+                       const float* mu, const float* z, int t, int n, void* stream);
+
+/* Workload model: algorithmic FLOPs of one UNet forward at (B,H,W) and of one encode,
+ * counted 2*MAC over conv/linear/bmm like torch.utils.flop_counter. */
+double dac_unet_flops(dac_handle* h, int B, int H, int W);
+double dac_encode_flops(dac_handle* h, int B);
+
+/* Kernel timing over the next dac_sde_reverse call: HIP events around every launch of
+ * the dominant conv class (`kernel_id` = 0), on the stream it runs on. Returns the
+ * number of timed launches and their mean duration (ms) / flops per launch. */
+int dac_profile_enable(dac_handle* h, int kernel_id);
+int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
+                     double* bytes_per_launch);
+
+const char* dac_last_error(dac_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DACLIP_HIP_H */

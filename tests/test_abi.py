@@ -1,0 +1,40 @@
+"""CPU-side checks of the C ABI: the built library loads and exports every function
+include/daclip_hip.h declares (no compute calls without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared():
+    src = open(os.path.join(ROOT, "include", "daclip_hip.h")).read()
+    return sorted(set(re.findall(r"\b(dac_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_abi():
+    names = declared()
+    for n in ("dac_create", "dac_set_weight", "dac_finalize_weights", "dac_encode_image",
+              "dac_unet_forward", "dac_sde_reverse", "dac_last_error"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from daclip_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libdaclip_hip.so not built")
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared() if not hasattr(L, n)]
+    assert not missing
+    assert sorted(_lib.EXPORTS) == declared()
+
+
+def test_create_without_gpu_fails_cleanly():
+    import torch
+    from daclip_amd import _lib
+    if torch.cuda.is_available() or not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("CPU-only check")
+    with pytest.raises(RuntimeError, match="GPU"):
+        _lib.Handle(torch.device("cuda", 0), "fp32", _lib.DacConfig())
