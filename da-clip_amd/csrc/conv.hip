@@ -31,10 +31,12 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int M = a.B * a.Ho * a.Wo;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int slot = tid & 7, rbase = tid >> 3;
   const int HWo = a.Ho * a.Wo;
+  // Batched grid (per-image weights): rows of image blockIdx.z only.
+  const bool batched = a.w_bstride > 0;
+  const int M = batched ? (blockIdx.z + 1) * HWo : a.B * HWo;
+  const int m0 = (batched ? blockIdx.z * HWo : 0) + blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int slot = tid & 7, rbase = tid >> 3;
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
 
   // Per-thread A rows: output pixel -> (image base, top-left input coordinate).
@@ -54,7 +56,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
   }
   const T* x1 = reinterpret_cast<const T*>(a.x1);
   const T* x2 = reinterpret_cast<const T*>(a.x2);
-  const T* wgt = reinterpret_cast<const T*>(a.w);
+  const T* wgt = reinterpret_cast<const T*>(a.w) + (batched ? blockIdx.z * a.w_bstride : 0);
 
   u32x4 ra[AV], rb[BV];
   const int nk = (a.K + BKE - 1) / BKE;
@@ -77,6 +79,28 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
         v = *reinterpret_cast<const u32x4*>(src);
       }
       ra[i] = v;
+    }
+    if (a.amode == 1) {
+      // softmax over the 32 channels of each head (32/VE lanes of one row share a head).
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        float f[VE];
+        const T* e = reinterpret_cast<const T*>(&ra[i]);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { f[j] = to_f(e[j]); mx = fmaxf(mx, f[j]); }
+#pragma unroll
+        for (int o = 1; o < 32 / VE; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { f[j] = expf(f[j] - mx); sm += f[j]; }
+#pragma unroll
+        for (int o = 1; o < 32 / VE; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const float inv = 1.f / sm;
+        T* w = reinterpret_cast<T*>(&ra[i]);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) w[j] = from_f<T>(f[j] * inv * 0.17677669529663687f);
+      }
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
@@ -184,14 +208,17 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 template <typename T, int KH, int KW, int S, int P>
 static void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
+  const bool batched = a.w_bstride > 0;
+  const int Mg = batched ? a.Ho * a.Wo : M;
+  const int gz = batched ? a.B : 1;
   if (a.Cout <= 16 && a.act != ACT_GEGLU) {
-    dim3 g((M + 255) / 256, (a.Cout + 15) / 16);
+    dim3 g((Mg + 255) / 256, (a.Cout + 15) / 16, gz);
     conv_kernel<T, 256, 16, 4, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
   } else if (a.Cout <= 64) {
-    dim3 g((M + 255) / 256, (a.Cout + 63) / 64);
+    dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, gz);
     conv_kernel<T, 256, 64, 4, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
   } else {
-    dim3 g((M + 127) / 128, (a.Cout + 127) / 128);
+    dim3 g((Mg + 127) / 128, (a.Cout + 127) / 128, gz);
     conv_kernel<T, 128, 128, 2, 2, KH, KW, S, P><<<g, 256, 0, st>>>(a);
   }
 }

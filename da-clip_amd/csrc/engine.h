@@ -103,6 +103,8 @@ struct Epi {
   const void* res2 = nullptr; int ldr2 = 0;
   const float* bbias = nullptr; int bb_ld = 0;
   int act = ACT_NONE;
+  int amode = 0;                 // A-loader transform (ConvArgs::amode)
+  long long w_bstride = 0;       // per-image weights (ConvArgs::w_bstride)
 };
 
 int conv_tile_id(int cout, int act);

@@ -29,6 +29,11 @@ struct ConvArgs {
   const float* bbias; int bb_ld;   // per-image bias [b*bb_ld + n]; or null
   void* y; int ldy;
   int act;
+  // A-loader transform: 0 none; 1 = LinearAttention q path: softmax over each 32-channel
+  // head group then * 32^-0.5 (module_util.py:175, 177).
+  int amode;
+  // > 0: per-image weights W + b * w_bstride (grid.z = B, tiles never straddle images).
+  long long w_bstride;
 };
 
 template <typename T>
@@ -54,12 +59,16 @@ void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, 
 template <typename T>
 void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t st);
 
-// LinearAttention (module_util.py:170-185) on qkv [B*HW, 384]:
-//   kernel 1: per (image, pixel chunk) partial k-softmax stats and k v^T context
-//   kernel 2: combine chunks -> ctx[b][h][d][e]  (already / sum_k and / HW)
-//   kernel 3: out[n, h*32+e] = scale * sum_d ctx[d][e] * softmax_d(q)[d]
+// LinearAttention (module_util.py:170-185) context on qkv [B*HW, 384] (q | k | v):
+//   la_kmax   : per (image, chunk) channel max of k
+//   la_ctx    : per (image, chunk) sum_n exp(k - max) v^T on MFMA (+ exp sums)
+//   la_reduce : merge chunk partials in fixed order (deterministic)
+//   la_weff   : W_eff[b][c][h*32+d] = sum_e Wout[c][h*32+e] ctx[b][h][d][e] / sum / HW
+// The to_out 1x1 conv then runs as a GEMM of softmax_d(q)*scale (fused into its A loader,
+// amode = 1) with the per-image W_eff: Wout (ctx^T q) = (Wout ctx^T) q.
 template <typename T>
-void linear_attention(const void* qkv, void* out, int B, int HW, float* ws, hipStream_t st);
+void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
+                           float* ws, hipStream_t st);
 size_t linear_attention_ws_floats(int B, int HW);
 
 // Small fp32 dense layer for per-image vectors (time / prompt MLPs, ViT head):
