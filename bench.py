@@ -35,8 +35,8 @@ def parse():
     p.add_argument("--res", type=int, default=256)
     p.add_argument("--T", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--kernel-id", type=int, default=301,
-                   help="conv class timed for the roofline (kh*100 + tile; 301 = 3x3, 256x64 tile)")
+    p.add_argument("--kernel-id", type=int, default=306,
+                   help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo 256x64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")
     return p.parse_args()

@@ -1,0 +1,136 @@
+// conv_epi.h — shared epilogue of the implicit-GEMM conv kernels.
+//
+// Phase 1 (registers): bias -> per-image scale/shift -> SiLU/GELU (or the GEGLU pairing of
+// accumulator tiles j, j+1) on each wave's TM x TN 16x16 accumulators, written as fp32 into
+// an LDS image of the block tile [BM][BN] (row pad 16 B: the 4 lane groups of a wave land on
+// disjoint bank quarters).
+// Phase 2 (coalesced): every thread moves 16-byte output chunks (VE channels of one row):
+// + res1 + res2 + per-image bias, one 16-byte store; rows map through `rowmap` (row-halo
+// tiles are 2-D in the image). Partial / misaligned chunks fall back to scalars.
+// Keeping the LDS image in fp32 keeps the residual adds in fp32 like the reference.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+namespace dac {
+
+struct LinearRows {      // block-tile row t -> output row m0 + t
+  int m0;
+  DEV int operator()(int t) const { return m0 + t; }
+};
+
+template <typename T> DEV float silu_t(float x);
+template <> DEV float silu_t<float>(float x) { return x / (1.f + expf(-x)); }
+template <> DEV float silu_t<bf16>(float x) { return x * __frcp_rn(1.f + __expf(-x)); }
+
+template <int BM, int BN>
+struct EpiLds {
+  static constexpr int LDW = BN + 4;                 // floats per LDS row
+  static constexpr int BYTES = BM * LDW * 4;
+};
+
+template <typename T, int BM, int BN, int WGM, int WGN, class RowMap>
+DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
+                           char* smem, int M, const RowMap& rowmap, int n0, int HWo) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int LDW = EpiLds<BM, BN>::LDW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const bool geglu = a.act == ACT_GEGLU;
+  float* tile = reinterpret_cast<float*>(smem);
+  __syncthreads();                                   // main-loop LDS reads are finished
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = wm * WTM + i * 16 + lg * 4 + r;
+      const int m = rowmap(t);
+      const int b = m < M ? m / HWo : 0;
+      float* row = tile + t * LDW;
+      if (geglu) {
+        if constexpr (TN % 2 == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; j += 2) {
+            const int cx = wn * WTN + j * 16 + lr;
+            const int nx = n0 + cx;
+            float vx = acc[i][j][r], vg = acc[i][j + 1][r];
+            if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
+            row[(wn * WTN + j * 16) / 2 + lr] = vx * gelu_f(vg);
+          }
+        }
+        continue;
+      }
+      const float* s = a.ss ? a.ss + (size_t)b * a.ss_ld : nullptr;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int c = wn * WTN + j * 16 + lr;
+        const int n = n0 + c;
+        float v = acc[i][j][r];
+        if (n < a.Cout) {
+          if (a.bias) v += a.bias[n];
+          if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
+        }
+        if (a.act == ACT_SILU) v = silu_t<T>(v);
+        else if (a.act == ACT_GELU) v = gelu_f(v);
+        row[c] = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int OW = geglu ? BN / 2 : BN;                // output tile width (channels)
+  const int Cout = geglu ? a.Cout / 2 : a.Cout;
+  const int nb = geglu ? n0 / 2 : n0;
+  const int CPR = OW / VE;                           // 16-byte chunks per tile row
+  T* y = reinterpret_cast<T*>(a.y);
+  const T* r1 = reinterpret_cast<const T*>(a.res1);
+  const T* r2 = reinterpret_cast<const T*>(a.res2);
+  const bool vec_ok = (a.ldy % VE == 0) && (!r1 || a.ldr1 % VE == 0) && (!r2 || a.ldr2 % VE == 0);
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int t = c / CPR, cc = (c - t * CPR) * VE;
+    const int m = rowmap(t);
+    const int n = nb + cc;
+    if (m >= M || n >= Cout) continue;
+    const float* src = tile + t * LDW + cc;
+    float v[VE];
+#pragma unroll
+    for (int e = 0; e < VE; e += 4) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(src + e);
+      v[e] = q[0]; v[e + 1] = q[1]; v[e + 2] = q[2]; v[e + 3] = q[3];
+    }
+    const int b = m / HWo;
+    if (vec_ok && n + VE <= Cout) {
+      float t1[VE];
+      if (r1) {
+        load_vec<T>(r1 + (size_t)m * a.ldr1 + n, t1);
+#pragma unroll
+        for (int e = 0; e < VE; ++e) v[e] += t1[e];
+      }
+      if (r2) {
+        load_vec<T>(r2 + (size_t)m * a.ldr2 + n, t1);
+#pragma unroll
+        for (int e = 0; e < VE; ++e) v[e] += t1[e];
+      }
+      if (a.bbias) {
+        const float* bb = a.bbias + (size_t)b * a.bb_ld + n;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) v[e] += bb[e];
+      }
+      store_vec<T>(y + (size_t)m * a.ldy + n, v);
+    } else {
+      for (int e = 0; e < VE && n + e < Cout; ++e) {
+        float u = v[e];
+        if (r1) u += to_f(r1[(size_t)m * a.ldr1 + n + e]);
+        if (r2) u += to_f(r2[(size_t)m * a.ldr2 + n + e]);
+        if (a.bbias) u += a.bbias[(size_t)b * a.bb_ld + n + e];
+        y[(size_t)m * a.ldy + n + e] = from_f<T>(u);
+      }
+    }
+  }
+}
+
+}  // namespace dac

@@ -1,0 +1,542 @@
+// conv_impl.h — MFMA implicit-GEMM convolution kernels for gfx950 (NHWC activations).
+//
+// One kernel covers every conv/linear of the hot path (SURVEY.md §2.3 op census):
+// conv3x3 s1 p1 (module_util.py:111-112), conv4x4 s2 p1 (Downsample, :107-108),
+// nearest-2x + conv3x3 (Upsample, :100-104), conv7x7 (init_conv), 1x1 convs / nn.Linear
+// (to_qkv, res_conv, proj_in/out, q/k/v/out, GEGLU, ViT projections) and the ViT 32x32/s32
+// patch embedding (transformer.py:411).
+//
+// Tiling: 256 threads = 4 waves arranged WGM x WGN over a BM x BN output tile; each wave owns
+// a (BM/WGM) x (BN/WGN) sub-tile of 16x16 MFMA tiles. The K loop walks 128-byte K slices
+// (64 bf16 or 32 f32 per row) through double-buffered LDS; global->register prefetch of
+// slice k+1 overlaps the MFMAs of slice k. LDS rows are 128 B with the 16-byte slot
+// XOR-swizzled by (row>>1)&7 so the 16 rows read by a ds_read_b128 lane group hit distinct
+// banks.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+#include "conv_epi.h"
+
+namespace dac {
+
+// XCD-aware block order (cdna_hip_programming.md T1): the dispatcher deals blocks round-robin
+// over the 8 XCDs, so neighbouring output tiles (which share input rows / weights) would
+// sit in different L2s. Remap the linear block id bijectively so each XCD walks a
+// contiguous range of (n-tile fastest, then m-tile, then image) tiles. Speed only.
+struct TileId { int bx, by, bz; };
+DEV TileId xcd_tile() {
+  const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+  const int n = gx * gy * gz;
+  const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = n / 8, r = n % 8, xcd = id % 8;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+  TileId o;
+  o.by = t % gy;
+  o.bx = (t / gy) % gx;
+  o.bz = t / (gy * gx);
+  return o;
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN, int KH, int KW, int S, int P>
+__global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int BKE = 128 / sizeof(T);
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int AV = BM / 32;
+  constexpr int BV = (BN + 31) / 32;
+  constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
+  static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "tile");
+  constexpr int SMEM = 2 * (BM + BN) * 128 > EpiLds<BM, BN>::BYTES ? 2 * (BM + BN) * 128
+                                                                   : EpiLds<BM, BN>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int HWo = a.Ho * a.Wo;
+  const TileId tl = xcd_tile();
+  // Batched grid (per-image weights): rows of image tl.bz only.
+  const bool batched = a.w_bstride > 0;
+  const int M = batched ? (tl.bz + 1) * HWo : a.B * HWo;
+  const int m0 = (batched ? tl.bz * HWo : 0) + tl.bx * BM, n0 = tl.by * BN;
+  const int slot = tid & 7, rbase = tid >> 3;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+
+  // Per-thread A rows: output pixel -> (image base, top-left input coordinate).
+  int a_pix[AV], a_ih[AV], a_iw[AV];
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    int m = m0 + rbase + 32 * i;
+    if (m < M) {
+      int b = m / HWo, r = m - b * HWo;
+      int oh = r / a.Wo, ow = r - oh * a.Wo;
+      a_pix[i] = b * a.Hs * a.Ws;
+      a_ih[i] = oh * S - P;
+      a_iw[i] = ow * S - P;
+    } else {
+      a_pix[i] = 0; a_ih[i] = -100000; a_iw[i] = -100000;
+    }
+  }
+  const T* x1 = reinterpret_cast<const T*>(a.x1);
+  const T* x2 = reinterpret_cast<const T*>(a.x2);
+  const T* wgt = reinterpret_cast<const T*>(a.w) + (batched ? tl.bz * a.w_bstride : 0);
+
+  u32x4 ra[AV], rb[BV];
+  const int nk = (a.K + BKE - 1) / BKE;
+
+  auto gload = [&](int kt) {
+    const int k = kt * BKE + slot * VE;
+    const bool kv = k < a.K;
+    int kpos = k / a.Cin;
+    const int ci = k - kpos * a.Cin;
+    const int kh = kpos / KW, kw = kpos - (kpos / KW) * KW;
+    const bool from1 = ci < a.C1;
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (kv && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win) {
+        const int sh = a.up ? (ih >> 1) : ih, sw = a.up ? (iw >> 1) : iw;
+        const size_t pix = (size_t)(a_pix[i] + sh * a.Ws + sw);
+        const T* src = from1 ? x1 + pix * a.ld1 + ci : x2 + pix * a.ld2 + (ci - a.C1);
+        v = *reinterpret_cast<const u32x4*>(src);
+      }
+      ra[i] = v;
+    }
+    if (a.amode == 1) {
+      // softmax over the 32 channels of each head (32/VE lanes of one row share a head).
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        float f[VE];
+        const T* e = reinterpret_cast<const T*>(&ra[i]);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { f[j] = to_f(e[j]); mx = fmaxf(mx, f[j]); }
+#pragma unroll
+        for (int o = 1; o < 32 / VE; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) { f[j] = expf(f[j] - mx); sm += f[j]; }
+#pragma unroll
+        for (int o = 1; o < 32 / VE; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const float inv = 1.f / sm;
+        T* w = reinterpret_cast<T*>(&ra[i]);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) w[j] = from_f<T>(f[j] * inv * 0.17677669529663687f);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int r = rbase + 32 * i;
+      const int n = n0 + r;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (r < BN && n < a.Cout && kv) v = *reinterpret_cast<const u32x4*>(wgt + (size_t)n * a.K + k);
+      rb[i] = v;
+    }
+  };
+  auto swz = [](int row, int s) { return row * 128 + ((s ^ ((row >> 1) & 7)) << 4); };
+  auto swrite = [&](int buf) {
+    char* A = smem + buf * (BM + BN) * 128;
+    char* Bs = A + BM * 128;
+#pragma unroll
+    for (int i = 0; i < AV; ++i) *reinterpret_cast<u32x4*>(A + swz(rbase + 32 * i, slot)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int r = rbase + 32 * i;
+      if (r < BN) *reinterpret_cast<u32x4*>(Bs + swz(r, slot)) = rb[i];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int lr = lane & 15, lg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* A = smem + cur * (BM + BN) * 128;
+    const char* Bs = A + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      u32x4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const u32x4*>(A + swz(wm * WTM + i * 16 + lr, ks * 4 + lg));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const u32x4*>(Bs + swz(wn * WTN + j * 16 + lr, ks * 4 + lg));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// v2: NW = WGM*WGN waves, STAGES-deep LDS ring filled by global_load_lds (LDS-DMA, 16 B per
+// lane, no register staging). Padding rows / K tail read a 16-byte zero page. The LDS image
+// is lane-linear per wave-instruction (8 rows x 128 B), so the (row>>1)&7 slot swizzle is
+// applied on the SOURCE address: lane l fills physical slot l&7 with logical slot
+// (l&7) ^ ((row>>1)&7). Per K tile: wait own DMA of tile kt (counted vmcnt), barrier, refill
+// the slot read in the previous iteration with tile kt+STAGES-1, then MFMA on tile kt.
+// Requires Cin % (128/sizeof(T)) == 0 so a K tile covers one (kh, kw) tap.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+template <typename T, int BM, int BN, int WGM, int WGN, int STAGES, int KH, int KW, int S, int P>
+__global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
+  constexpr int NW = WGM * WGN;
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int BKE = 128 / sizeof(T);
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int AG = BM / (8 * NW), BG = BN / (8 * NW);
+  constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
+  constexpr int STAGE = (BM + BN) * 128;
+  static_assert(AG >= 1 && BG >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
+  constexpr int SMEM = STAGES * STAGE > EpiLds<BM, BN>::BYTES ? STAGES * STAGE : EpiLds<BM, BN>::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int HWo = a.Ho * a.Wo;
+  const TileId tl = xcd_tile();
+  const bool batched = a.w_bstride > 0;
+  const int M = batched ? (tl.bz + 1) * HWo : a.B * HWo;
+  const int m0 = (batched ? tl.bz * HWo : 0) + tl.bx * BM, n0 = tl.by * BN;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  const T* x1 = reinterpret_cast<const T*>(a.x1);
+  const T* x2 = reinterpret_cast<const T*>(a.x2);
+  const T* wgt = reinterpret_cast<const T*>(a.w) + (batched ? tl.bz * a.w_bstride : 0);
+
+  // This lane's rows: A row (wave*AG + j)*8 + lane/8, B row (wave*BG + j)*8 + lane/8.
+  int a_pix[AG], a_ih[AG], a_iw[AG], a_ls[AG];
+#pragma unroll
+  for (int j = 0; j < AG; ++j) {
+    const int row = (wave * AG + j) * 8 + (lane >> 3);
+    a_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    if (m < M) {
+      const int b = m / HWo, r = m - b * HWo;
+      const int oh = r / a.Wo, ow = r - oh * a.Wo;
+      a_pix[j] = b * a.Hs * a.Ws;
+      a_ih[j] = oh * S - P;
+      a_iw[j] = ow * S - P;
+    } else {
+      a_pix[j] = 0; a_ih[j] = -100000; a_iw[j] = -100000;
+    }
+  }
+  const T* b_row[BG];
+  int b_ls[BG];
+#pragma unroll
+  for (int j = 0; j < BG; ++j) {
+    const int row = (wave * BG + j) * 8 + (lane >> 3);
+    b_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
+  }
+  const int nk = (a.K + BKE - 1) / BKE;
+
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % STAGES) * STAGE;
+    const int k0 = kt * BKE;
+    const bool kv = k0 < a.K;
+    const int kpos = k0 / a.Cin;                 // wave-uniform (Cin % BKE == 0)
+    const int ci0 = k0 - kpos * a.Cin;
+    const int kh = kpos / KW, kw = kpos - (kpos / KW) * KW;
+#pragma unroll
+    for (int j = 0; j < AG; ++j) {
+      const int ih = a_ih[j] + kh, iw = a_iw[j] + kw;
+      const int ci = ci0 + a_ls[j] * VE;
+      const char* src = zero;
+      if (kv && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win) {
+        const int sh = a.up ? (ih >> 1) : ih, sw = a.up ? (iw >> 1) : iw;
+        const size_t pix = (size_t)(a_pix[j] + sh * a.Ws + sw);
+        src = reinterpret_cast<const char*>(ci < a.C1 ? x1 + pix * a.ld1 + ci
+                                                      : x2 + pix * a.ld2 + (ci - a.C1));
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+      const char* src = zero;
+      if (kv && b_row[j]) src = reinterpret_cast<const char*>(b_row[j] + k0 + b_ls[j] * VE);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(st + BM * 128 + (wave * BG + j) * 8 * 128),
+                                       16, 0, 0);
+    }
+  };
+  auto swz = [](int row, int s) { return row * 128 + ((s ^ ((row >> 1) & 7)) << 4); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) issue(s);
+  const int lr = lane & 15, lg = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    // Own DMA of tile kt done (STAGES-2 younger tiles may stay in flight), then barrier.
+    if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(AG + BG) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * (AG + BG)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(kt + STAGES - 1);                      // refills the slot read at iteration kt-1
+    const char* A = smem + (kt % STAGES) * STAGE;
+    const char* Bs = A + BM * 128;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      u32x4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const u32x4*>(A + swz(wm * WTM + i * 16 + lr, ks * 4 + lg));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const u32x4*>(Bs + swz(wn * WTN + j * 16 + lr, ks * 4 + lg));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// v3 (3x3, stride 1, pad 1): row-halo tiles. A block owns BM output pixels laid out as
+// RH image rows x RW columns (RW = min(Wo, 256), power of two >= 16). The K loop walks
+// (Cin chunk of 128 B, kh): each stage holds the RH input rows (ih = oh + kh - 1) over
+// RW + 2 columns once, and the three kw taps read shifted windows of it, so every input
+// pixel of a row band is fetched once per kh instead of once per tap (im2col x3 -> x1).
+// The stage also holds the 3 (kw) weight tiles. Two LDS stages, LDS-DMA fill.
+// Row width of a v3 tile of BM pixels for this output, or 0 if the shape does not tile.
+inline int conv3_rw(const ConvArgs& a, int BM = 256) {
+  const int Wo = a.Wo, Ho = a.Ho;
+  if (Wo <= 0 || (Wo & (Wo - 1))) {
+    if (Wo % BM == 0) return BM;
+    return 0;
+  }
+  const int RW = Wo < BM ? Wo : BM;
+  if (RW < 16) return 0;
+  const int RH = BM / RW;
+  if (Ho % RH) return 0;
+  return RW;
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
+  constexpr int NW = WGM * WGN;
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int BKE = 128 / sizeof(T);
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int NPIX_MAX = BM + 2 * (BM / 16);           // RH * (RW + 2) with RW >= 16
+  constexpr int AG = (NPIX_MAX + 8 * NW - 1) / (8 * NW);
+  constexpr int BG = 3 * BN / (8 * NW);
+  constexpr int AROWS = AG * 8 * NW;
+  constexpr int STAGE = (AROWS + 3 * BN) * 128;
+  constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
+  static_assert(BG >= 1 && (3 * BN) % (8 * NW) == 0, "tile");
+  constexpr int SMEM = 2 * STAGE > EpiLds<BM, BN>::BYTES ? 2 * STAGE : EpiLds<BM, BN>::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int HWo = a.Ho * a.Wo;
+  const int RH = BM / RW, RWP = RW + 2, NPIX = RH * RWP;
+  const TileId tl = xcd_tile();
+  const int tiles_w = a.Wo / RW;
+  const int b = tl.bx / ((a.Ho / RH) * tiles_w);
+  const int tr = tl.bx - b * (a.Ho / RH) * tiles_w;
+  const int oh0 = (tr / tiles_w) * RH, ow0 = (tr % tiles_w) * RW;
+  const int n0 = tl.by * BN;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  const T* x1 = reinterpret_cast<const T*>(a.x1);
+  const T* x2 = reinterpret_cast<const T*>(a.x2);
+  const T* wgt = reinterpret_cast<const T*>(a.w);
+  const int pixb = b * a.Hs * a.Ws;
+
+  // A rows of this lane: stage pixel p -> (oy, ox) with input column ow0 + ox - 1.
+  int a_oy[AG], a_iw[AG], a_ls[AG];
+#pragma unroll
+  for (int j = 0; j < AG; ++j) {
+    const int p = (wave * AG + j) * 8 + (lane >> 3);
+    a_ls[j] = (lane & 7) ^ ((p >> 1) & 7);
+    if (p < NPIX) {
+      a_oy[j] = p / RWP;
+      a_iw[j] = ow0 + (p - a_oy[j] * RWP) - 1;
+    } else {
+      a_oy[j] = -100000; a_iw[j] = -100000;
+    }
+  }
+  const T* b_row[BG];
+  int b_ls[BG], b_kw[BG];
+#pragma unroll
+  for (int j = 0; j < BG; ++j) {
+    const int row = (wave * BG + j) * 8 + (lane >> 3);
+    b_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
+    b_kw[j] = row / BN;
+    const int n = n0 + row % BN;
+    b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
+  }
+  const int nchunk = a.Cin / BKE;
+  const int nst = nchunk * 3;
+
+  auto issue = [&](int s) {
+    char* st = smem + (s & 1) * STAGE;
+    const int c = s / 3, kh = s - c * 3;
+    const int ci0 = c * BKE;
+    const bool from1 = ci0 < a.C1;
+    const T* xs = from1 ? x1 : x2;
+    const int ld = from1 ? a.ld1 : a.ld2;
+    const int cb = from1 ? ci0 : ci0 - a.C1;
+#pragma unroll
+    for (int j = 0; j < AG; ++j) {
+      const int ih = oh0 + a_oy[j] + kh - 1, iw = a_iw[j];
+      const char* src = zero;
+      if ((unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win) {
+        const int sh = a.up ? (ih >> 1) : ih, sw = a.up ? (iw >> 1) : iw;
+        src = reinterpret_cast<const char*>(xs + (size_t)(pixb + sh * a.Ws + sw) * ld + cb +
+                                            a_ls[j] * VE);
+      }
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+      const char* src = zero;
+      if (b_row[j])
+        src = reinterpret_cast<const char*>(b_row[j] + (kh * 3 + b_kw[j]) * a.Cin + ci0 + b_ls[j] * VE);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                       (lds_void_t*)(st + AROWS * 128 + (wave * BG + j) * 8 * 128),
+                                       16, 0, 0);
+    }
+  };
+  auto swz = [](int row, int s) { return row * 128 + ((s ^ ((row >> 1) & 7)) << 4); };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  // Stage pixel of this lane's A fragment rows (tap kw = 0).
+  int a_pix[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WTM + i * 16 + lr;
+    const int oy = r / RW;
+    a_pix[i] = oy * RWP + (r - oy * RW);
+  }
+  issue(0);
+  for (int s = 0; s < nst; ++s) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 1 < nst) issue(s + 1);               // refills the stage read at step s-1
+    const char* A = smem + (s & 1) * STAGE;
+    const char* Bs = A + AROWS * 128;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        u32x4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const u32x4*>(A + swz(a_pix[i] + kw, ks * 4 + lg));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const u32x4*>(Bs + swz(kw * BN + wn * WTN + j * 16 + lr, ks * 4 + lg));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+      }
+    }
+  }
+  struct Rows {
+    int base, RW, Wo;
+    DEV int operator()(int t) const {
+      const int oy = t / RW;
+      return base + oy * Wo + (t - oy * RW);
+    }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const Rows rm{b * HWo + oh0 * a.Wo + ow0, RW, a.Wo};
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo);
+}
+
+template <typename T, int KH, int KW, int S, int P>
+void conv_dispatch(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.Ho * a.Wo;
+  const bool batched = a.w_bstride > 0;
+  const int Mg = batched ? a.Ho * a.Wo : M;
+  const int gz = batched ? a.B : 1;
+  constexpr int BKE = 128 / sizeof(T);
+  // Tap shapes whose Cin is always a multiple of the K tile use v2; v1 serves the rest
+  // (init conv Cin=8, patch embed, final conv Cout=3, LinearAttention to_out amode=1).
+  constexpr bool V2 = (KH == 1 || KH == 3 || KH == 4);
+  const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
+    const int RW = conv3_rw(a);
+    if (v2ok && RW > 0 && a.w_bstride == 0) {
+      if (a.Cout <= 64) {
+        dim3 g(a.B * a.Ho * a.Wo / 256, (a.Cout + 63) / 64, 1);
+        conv3_kernel<T, 256, 64, 4, 2><<<g, 512, 0, st>>>(a, RW);
+        return;
+      }
+      if (conv3_rw(a, 128) > 0) {
+        dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 127) / 128, 1);
+        conv3_kernel<T, 128, 128, 2, 4><<<g, 512, 0, st>>>(a, conv3_rw(a, 128));
+        return;
+      }
+    }
+  }
+  if constexpr (V2) if (v2ok) {
+    if (a.Cout <= 64) {
+      dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, gz);
+      conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P><<<g, 512, 0, st>>>(a);
+    } else if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) {
+      dim3 g((Mg + 255) / 256, (a.Cout + 127) / 128, gz);
+      conv2_kernel<T, 256, 128, 4, 2, 3, KH, KW, S, P><<<g, 512, 0, st>>>(a);
+    } else {
+      dim3 g((Mg + 127) / 128, (a.Cout + 127) / 128, gz);
+      conv2_kernel<T, 128, 128, 2, 2, 3, KH, KW, S, P><<<g, 256, 0, st>>>(a);
+    }
+    return;
+  }
+  if (a.Cout <= 16 && a.act != ACT_GEGLU) {
+    dim3 g((Mg + 255) / 256, (a.Cout + 15) / 16, gz);
+    conv_kernel<T, 256, 16, 4, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
+  } else if (a.Cout <= 64) {
+    dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, gz);
+    conv_kernel<T, 256, 64, 4, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
+  } else {
+    dim3 g((Mg + 127) / 128, (a.Cout + 127) / 128, gz);
+    conv_kernel<T, 128, 128, 2, 2, KH, KW, S, P><<<g, 256, 0, st>>>(a);
+  }
+}
+
+
+}  // namespace dac

@@ -1,0 +1,7 @@
+// conv_k1.hip — explicit instantiations of the implicit-GEMM conv (split for parallel builds).
+#include "conv_impl.h"
+
+namespace dac {
+template void conv_dispatch<float, 1, 1, 1, 0>(const ConvArgs&, hipStream_t);
+template void conv_dispatch<bf16, 1, 1, 1, 0>(const ConvArgs&, hipStream_t);
+}  // namespace dac

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace dac {
 
@@ -136,12 +137,6 @@ struct Packer {
 };
 
 // ============================================================================= launches
-int conv_tile_id(int cout, int act) {
-  if (cout <= 16 && act != ACT_GEGLU) return 0;
-  if (cout <= 64) return 1;
-  return 2;
-}
-
 Profiler::~Profiler() {
   for (auto e : ev) (void)hipEventDestroy(e);
 }
@@ -159,12 +154,12 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.Cout = cw.cout; a.K = cw.kh * cw.kw * cw.cin; a.w = cw.w; a.bias = cw.b;
   a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
-  a.amode = e.amode; a.w_bstride = e.w_bstride;
+  a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero;
   const double M = (double)B * a.Ho * a.Wo;
   const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   r.flops += fl;
   Profiler* p = r.prof;
-  const bool timed = p && p->kernel_id == cw.kh * 100 + conv_tile_id(cw.cout, e.act);
+  const bool timed = p && p->kernel_id == cw.kh * 100 + conv_variant(a, cw.kh, (int)sizeof(T));
   if (r.dry) {
     if (timed) p->used++;
     return;
@@ -400,11 +395,12 @@ struct UNetNet {
   }
 
   // ----------------------------------------------------------------- per-call tables
-  // ss_all[(i*B + b)*ss_total + off ...]: ResBlock (scale, shift) for step i, image b.
-  // sin_tab: [nT*B][nf] sinusoidal embeddings (row i*B+b = step i).
-  void tables(Run& r, const float* sin_tab, int nT, const float* tc, const float* icx, int B,
-              float* ss_all, float* cc) {
+  // ss_all[(i*B + b)*ss_total + off ...]: ResBlock (scale, shift) for step i, image b, whose
+  // time is t0 + dt * i. sin_tab: [nT*B][nf] device scratch for the sinusoidal embeddings.
+  void tables(Run& r, float* sin_tab, int nT, float t0, float dt, const float* tc,
+              const float* icx, int B, float* ss_all, float* cc) {
     const int R = nT * B;
+    if (!r.dry) sinus_embedding(sin_tab, R, B, nf, t0, dt, r.st);
     float* h1 = r.alloc<float>((size_t)R * tdim);
     float* temb = r.alloc<float>((size_t)R * tdim);
     float* pe = nullptr;
@@ -726,6 +722,8 @@ class EngineT : public Engine {
     HIP_OK(hipStreamCreateWithFlags(&priv, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+    zero_page = pool.alloc(256);
+    HIP_OK(hipMemset(zero_page, 0, 256));
     if (c.unet) unet = std::make_unique<UNetNet<T>>(c);
     if (c.vit) {
       if (c.image_size % c.patch_size || c.width % c.head_width || c.head_width > 64 ||
@@ -764,6 +762,7 @@ class EngineT : public Engine {
     arena.base = nullptr;
     HIP_OK(hipMalloc(&arena.base, bytes));
     arena.cap = bytes;
+    if (poison()) HIP_OK(hipMemset(arena.base, 0xFF, bytes));
   }
   struct Bufs {
     float *xs = nullptr, *mus = nullptr, *tcs = nullptr, *ics = nullptr, *ss = nullptr,
@@ -778,27 +777,18 @@ class EngineT : public Engine {
                     (void*)b.cc, (void*)b.sin, b.out, (void*)b.seed})
       if (p) (void)hipFree(p);
   }
+  // DAC_POISON=1: fill fresh workspace with 0xFF bytes (NaN in f32/bf16) so any
+  // read-before-write shows up as a NaN in the outputs (debug aid).
+  static bool poison() {
+    static const bool p = getenv("DAC_POISON") && getenv("DAC_POISON")[0] == '1';
+    return p;
+  }
   template <class X> X* dalloc(size_t n) {
     void* p = nullptr;
-    HIP_OK(hipMalloc(&p, std::max<size_t>(n * sizeof(X), 16)));
+    const size_t bytes = std::max<size_t>(n * sizeof(X), 16);
+    HIP_OK(hipMalloc(&p, bytes));
+    if (poison()) HIP_OK(hipMemset(p, 0xFF, bytes));
     return (X*)p;
-  }
-  // Sinusoidal time embedding rows [nT*B][nf] for t = times[i] (SinusoidalPosEmb,
-  // module_util.py:41-48, fp32).
-  std::vector<float> sin_table(const std::vector<float>& times, int B) {
-    const int nf = unet->nf, half = nf / 2;
-    const float emb = (float)(std::log(10000.0) / (half - 1));
-    std::vector<float> tab((size_t)times.size() * B * nf);
-    for (size_t i = 0; i < times.size(); ++i)
-      for (int b = 0; b < B; ++b)
-        for (int k = 0; k < half; ++k) {
-          const float f = std::exp((float)k * -emb);
-          const float a = times[i] * f;
-          float* row = tab.data() + (i * B + b) * nf;
-          row[k] = std::sin(a);
-          row[half + k] = std::cos(a);
-        }
-    return tab;
   }
   Bufs& get_bufs(int B, int H, int W, int nT) {
     auto key = std::make_tuple(B, H, W, nT);
@@ -825,7 +815,7 @@ class EngineT : public Engine {
     Run r;
     r.dry = true;
     r.ar = &a;
-    unet->tables(r, nullptr, nT, (const float*)1, (const float*)1, B, nullptr, nullptr);
+    unet->tables(r, nullptr, nT, 0.f, 0.f, (const float*)1, (const float*)1, B, nullptr, nullptr);
     const size_t t = a.peak;
     a.reset();
     unet->forward(r, nullptr, nullptr, B, H, W, nullptr, nullptr, nullptr, 4);
@@ -834,6 +824,7 @@ class EngineT : public Engine {
   Run live(hipStream_t st) {
     Run r;
     r.st = st;
+    r.zero = zero_page;
     r.dry = false;
     arena.dry = false;
     r.ar = &arena;
@@ -864,11 +855,9 @@ class EngineT : public Engine {
     HIP_OK(hipSetDevice(dev));
     ensure_arena(plan_unet(B, H, W, 1));
     Bufs& b = get_bufs(B, H, W, 1);
-    auto tab = sin_table({t}, B);
-    HIP_OK(hipMemcpyAsync(b.sin, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, st));
     Run r = live(st);
     arena.reset();
-    unet->tables(r, b.sin, 1, tc, icx, B, b.ss, b.cc);
+    unet->tables(r, b.sin, 1, t, 0.f, tc, icx, B, b.ss, b.cc);
     arena.reset();
     unet->forward(r, xt, mu, B, H, W, b.ss, b.cc, b.out, b.ldo);
     unet_out<T>(b.out, b.ldo, eps, B, H, W, unet->pad_of(H), unet->pad_of(W), st);
@@ -901,7 +890,7 @@ class EngineT : public Engine {
   void record_loop(Run& r, Bufs& b, int mode, int B, int H, int W, int nT, const float* noise) {
     const int Hp = unet->pad_of(H), Wp = unet->pad_of(W);
     r.ar->reset();
-    unet->tables(r, b.sin, nT, b.tcs, b.ics, B, b.ss, b.cc);
+    unet->tables(r, b.sin, nT, (float)nT, -1.f, b.tcs, b.ics, B, b.ss, b.cc);
     const size_t n = (size_t)B * 3 * H * W;
     for (int i = 0; i < nT; ++i) {
       const int t = nT - i;
@@ -930,11 +919,7 @@ class EngineT : public Engine {
     if (icx) HIP_OK(hipMemcpyAsync(b.ics, icx, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
     seed_host = seed;
     HIP_OK(hipMemcpyAsync(b.seed, &seed_host, 8, hipMemcpyHostToDevice, priv));
-    std::vector<float> times;
-    for (int i = 0; i < nT; ++i) times.push_back((float)(nT - i));
-    auto tab = sin_table(times, B);
-    HIP_OK(hipMemcpyAsync(b.sin, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, priv));
-    HIP_OK(hipStreamSynchronize(priv));       // host staging buffers above are pageable
+    HIP_OK(hipStreamSynchronize(priv));       // seed_host staging is pageable
     // tc == nullptr is a different program (no prompt embedding): key it via mode bit.
     const int mkey = mode | (tc ? 0 : 2);
     if (prof.kernel_id >= 0) {
@@ -946,6 +931,7 @@ class EngineT : public Engine {
       d.dry = true;
       d.ar = &da;
       d.prof = &prof;
+      d.zero = zero_page;
       prof.begin_pass();
       record_loop(d, b, mode, B, H, W, nT, noise);
       while (prof.ev.size() < 2 * prof.used) {
@@ -1016,6 +1002,7 @@ class EngineT : public Engine {
   hipStream_t priv;
   hipEvent_t ev_in, ev_out;
   uint64_t seed_host = 0;
+  void* zero_page = nullptr;
 };
 
 std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {

@@ -78,7 +78,7 @@ struct Arena {
 };
 
 struct Profiler {
-  int kernel_id = -1;            // conv class to time (kh*100 + tile), -1 = off
+  int kernel_id = -1;            // conv class to time (kh*100 + conv_variant), -1 = off
   std::vector<hipEvent_t> ev;    // start/stop pairs
   size_t used = 0;               // pairs recorded in the current pass
   double flops = 0, bytes = 0;   // algorithmic work of the recorded launches
@@ -92,6 +92,7 @@ struct Run {
   bool dry = false;
   Arena* ar = nullptr;
   Profiler* prof = nullptr;
+  const void* zero = nullptr;    // 256 zero bytes on the device (conv padding source)
   double flops = 0;              // executed FLOPs (2*MAC) accumulated by the launches
   template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
 };
@@ -106,8 +107,6 @@ struct Epi {
   int amode = 0;                 // A-loader transform (ConvArgs::amode)
   long long w_bstride = 0;       // per-image weights (ConvArgs::w_bstride)
 };
-
-int conv_tile_id(int cout, int act);
 
 template <typename T>
 void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,

@@ -34,10 +34,12 @@ struct ConvArgs {
   int amode;
   // > 0: per-image weights W + b * w_bstride (grid.z = B, tiles never straddle images).
   long long w_bstride;
+  const void* zero;        // >= 16 zero bytes in global memory (source of padding rows)
 };
 
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
+int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 
 // Row LayerNorm over C (channel LN of NHWC == token LN):
 //   y = [res +] (x - mean) * rsqrt(var + eps) * g [+ b]
@@ -76,6 +78,8 @@ size_t linear_attention_ws_floats(int B, int HW);
 void small_linear(const float* x, int ldx, const float* W, const float* b, float* y, int ldy,
                   int R, int I, int O, int pre_act, int post_act, const float* add, int add_ld,
                   int add_mod, hipStream_t st);
+// out[r, :nf] = SinusoidalPosEmb(t0 + dt * (r / B)) for r < R (module_util.py:41-48).
+void sinus_embedding(float* out, int R, int B, int nf, float t0, float dt, hipStream_t st);
 // y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)
 void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st);
 

@@ -11,6 +11,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cmath>
+
 namespace dac {
 
 __device__ __forceinline__ float act_f(float v, int a) {
@@ -80,6 +82,25 @@ __global__ void __launch_bounds__(256) softmax_mul_kernel(const float* x, const 
 
 void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st) {
   softmax_mul_kernel<<<R, 256, 0, st>>>(x, v, y, C);
+}
+
+// SinusoidalPosEmb (module_util.py:41-48) for R = n_t * B rows: row r uses time
+// t0 + dt * (r / B); emb = exp(k * -(ln(10000) / (half - 1))) in fp32.
+__global__ void sinus_kernel(float* out, int R, int B, int nf, float t0, float dt, float negemb) {
+  const int half = nf / 2;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * half) return;
+  const int r = i / half, k = i - r * half;
+  const float t = t0 + dt * (float)(r / B);
+  const float a = t * expf((float)k * negemb);
+  out[(size_t)r * nf + k] = sinf(a);
+  out[(size_t)r * nf + half + k] = cosf(a);
+}
+
+void sinus_embedding(float* out, int R, int B, int nf, float t0, float dt, hipStream_t st) {
+  const int half = nf / 2;
+  const float negemb = (float)(-(std::log(10000.0) / (half - 1)));
+  sinus_kernel<<<(R * half + 255) / 256, 256, 0, st>>>(out, R, B, nf, t0, dt, negemb);
 }
 
 // --------------------------------------------------------------------------- UNet I/O

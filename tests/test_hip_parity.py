@@ -114,7 +114,8 @@ def test_python_loop_matches_native_loop(golden, unets):
     a = sde.reverse_posterior(noisy, T=5, noises=T(g["step_noise"][:5]), **kw)
     sde.set_model(lambda *x, **k: unets["fp32"](*x, **k))
     b = sde.reverse_posterior(noisy, T=5, noises=T(g["step_noise"][:5]), **kw)
-    assert rel(a.cpu().numpy(), b.cpu().numpy()) < 1e-5
+    r = rel(a.cpu().numpy(), b.cpu().numpy())
+    assert r < 1e-5, f"rel={r:.3e}"
 
 
 @pytest.mark.parametrize("name", ["daclip_small_encode.npz", "daclip_b32_encode.npz"])
