@@ -172,6 +172,7 @@ int dac_sde_schedule(dac_handle* h, float max_sigma, int T, int schedule, float 
   return guard(h, [&]() -> int {
     if (T < 1) throw dac::Error(DAC_E_ARG, "T must be >= 1");
     auto& s = h->eng->sched;
+    const dac::SdeSchedule old = s;
     dac::compute_schedule(s, max_sigma, T, schedule, eps);
     if (tables) {
       const int n = T + 1;
@@ -181,6 +182,9 @@ int dac_sde_schedule(dac_handle* h, float max_sigma, int T, int schedule, float 
       s.sbar.assign(tables + 3 * n, tables + 4 * n);
       s.dt = dt;
     }
+    if (s.T != old.T || s.dt != old.dt || s.max_sigma != old.max_sigma || s.thetas != old.thetas ||
+        s.sigmas != old.sigmas || s.tcum != old.tcum || s.sbar != old.sbar)
+      h->eng->invalidate_graphs();
     return DAC_OK;
   });
 }

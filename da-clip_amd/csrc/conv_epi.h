@@ -31,7 +31,7 @@ struct EpiLds {
 
 template <typename T, int BM, int BN, int WGM, int WGN, class RowMap>
 DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
-                           char* smem, int M, const RowMap& rowmap, int n0, int HWo) {
+                           char* smem, int M, const RowMap& rowmap, int n0, int HWo, int bimg) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
   constexpr int NT = 64 * WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
@@ -43,58 +43,82 @@ DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][
   float* tile = reinterpret_cast<float*>(smem);
   __syncthreads();                                   // main-loop LDS reads are finished
 
+  if (!geglu && bimg >= 0) {
+    // Fast path: all rows of the tile belong to image bimg -> per-channel terms in registers.
+    float sc[TN], sh[TN], bi[TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = wm * WTM + i * 16 + lg * 4 + r;
-      const int m = rowmap(t);
-      const int b = m < M ? m / HWo : 0;
-      float* row = tile + t * LDW;
-      if (geglu) {
-        if constexpr (TN % 2 == 0) {
-#pragma unroll
-          for (int j = 0; j < TN; j += 2) {
-            const int cx = wn * WTN + j * 16 + lr;
-            const int nx = n0 + cx;
-            float vx = acc[i][j][r], vg = acc[i][j + 1][r];
-            if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
-            row[(wn * WTN + j * 16) / 2 + lr] = vx * gelu_f(vg);
-          }
-        }
-        continue;
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + j * 16 + lr;
+      const bool ok = n < a.Cout;
+      bi[j] = (a.bias && ok) ? a.bias[n] : 0.f;
+      sc[j] = 1.f; sh[j] = 0.f;
+      if (a.ss && ok) {
+        const float* s = a.ss + (size_t)bimg * a.ss_ld;
+        sc[j] = s[n] + 1.f;
+        sh[j] = s[a.Cout + n];
       }
-      const float* s = a.ss ? a.ss + (size_t)b * a.ss_ld : nullptr;
+    }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int c = wn * WTN + j * 16 + lr;
-        const int n = n0 + c;
-        float v = acc[i][j][r];
-        if (n < a.Cout) {
-          if (a.bias) v += a.bias[n];
-          if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* row = tile + (wm * WTM + i * 16 + lg * 4 + r) * LDW + wn * WTN + lr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = (acc[i][j][r] + bi[j]) * sc[j] + sh[j];
+          if (a.act == ACT_SILU) v = silu_t<T>(v);
+          else if (a.act == ACT_GELU) v = gelu_f(v);
+          row[j * 16] = v;
         }
-        if (a.act == ACT_SILU) v = silu_t<T>(v);
-        else if (a.act == ACT_GELU) v = gelu_f(v);
-        row[c] = v;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = wm * WTM + i * 16 + lg * 4 + r;
+        const int m = rowmap(t);
+        const int b = bimg >= 0 ? bimg : (m < M ? m / HWo : 0);
+        float* row = tile + t * LDW;
+        if (geglu) {
+          if constexpr (TN % 2 == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; j += 2) {
+              const int cx = wn * WTN + j * 16 + lr;
+              const int nx = n0 + cx;
+              float vx = acc[i][j][r], vg = acc[i][j + 1][r];
+              if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
+              row[(wn * WTN + j * 16) / 2 + lr] = vx * gelu_f(vg);
+            }
+          }
+          continue;
+        }
+        const float* s = a.ss ? a.ss + (size_t)b * a.ss_ld : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int c = wn * WTN + j * 16 + lr;
+          const int n = n0 + c;
+          float v = acc[i][j][r];
+          if (n < a.Cout) {
+            if (a.bias) v += a.bias[n];
+            if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
+          }
+          if (a.act == ACT_SILU) v = silu_t<T>(v);
+          else if (a.act == ACT_GELU) v = gelu_f(v);
+          row[c] = v;
+        }
       }
     }
   }
   __syncthreads();
 
-  const int OW = geglu ? BN / 2 : BN;                // output tile width (channels)
-  const int Cout = geglu ? a.Cout / 2 : a.Cout;
-  const int nb = geglu ? n0 / 2 : n0;
-  const int CPR = OW / VE;                           // 16-byte chunks per tile row
   T* y = reinterpret_cast<T*>(a.y);
   const T* r1 = reinterpret_cast<const T*>(a.res1);
   const T* r2 = reinterpret_cast<const T*>(a.res2);
   const bool vec_ok = (a.ldy % VE == 0) && (!r1 || a.ldr1 % VE == 0) && (!r2 || a.ldr2 % VE == 0);
-  for (int c = tid; c < BM * CPR; c += NT) {
-    const int t = c / CPR, cc = (c - t * CPR) * VE;
+  auto emit = [&](int t, int cc, int n, int Cout) {
     const int m = rowmap(t);
-    const int n = nb + cc;
-    if (m >= M || n >= Cout) continue;
+    if (m >= M || n >= Cout) return;
     const float* src = tile + t * LDW + cc;
     float v[VE];
 #pragma unroll
@@ -102,7 +126,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][
       const f32x4 q = *reinterpret_cast<const f32x4*>(src + e);
       v[e] = q[0]; v[e + 1] = q[1]; v[e + 2] = q[2]; v[e + 3] = q[3];
     }
-    const int b = m / HWo;
+    const int b = bimg >= 0 ? bimg : m / HWo;
     if (vec_ok && n + VE <= Cout) {
       float t1[VE];
       if (r1) {
@@ -129,6 +153,24 @@ DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][
         if (a.bbias) u += a.bbias[(size_t)b * a.bb_ld + n + e];
         y[(size_t)m * a.ldy + n + e] = from_f<T>(u);
       }
+    }
+  };
+  if (!geglu) {
+    constexpr int CPR = BN / VE;                     // 16-byte chunks per tile row
+#pragma unroll
+    for (int k = 0; k < BM * CPR / NT; ++k) {
+      const int c = tid + k * NT;
+      const int t = c / CPR, cc = (c % CPR) * VE;
+      emit(t, cc, n0 + cc, a.Cout);
+    }
+  } else {
+    constexpr int CPR = BN / 2 / VE;
+#pragma unroll
+    for (int k = 0; k < (BM * CPR + NT - 1) / NT; ++k) {
+      const int c = tid + k * NT;
+      if (c >= BM * CPR) break;
+      const int t = c / CPR, cc = (c % CPR) * VE;
+      emit(t, cc, n0 / 2 + cc, a.Cout / 2);
     }
   }
 }

@@ -180,7 +180,9 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo);
+  const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
+  const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 
@@ -317,7 +319,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo);
+  const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
+  const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 
@@ -346,7 +350,8 @@ template <typename T, int BM, int BN, int WGM, int WGN>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
-  constexpr int BKE = 128 / sizeof(T);
+  constexpr int ES = sizeof(T);
+  constexpr int BKE = 128 / ES;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int NPIX_MAX = BM + 2 * (BM / 16);           // RH * (RW + 2) with RW >= 16
@@ -362,77 +367,93 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int HWo = a.Ho * a.Wo;
-  const int RH = BM / RW, RWP = RW + 2, NPIX = RH * RWP;
+  const int rws = __builtin_ctz(RW);                      // RW is a power of two
+  const int RH = BM >> rws, RWP = RW + 2, NPIX = RH * RWP;
   const TileId tl = xcd_tile();
-  const int tiles_w = a.Wo / RW;
-  const int b = tl.bx / ((a.Ho / RH) * tiles_w);
-  const int tr = tl.bx - b * (a.Ho / RH) * tiles_w;
-  const int oh0 = (tr / tiles_w) * RH, ow0 = (tr % tiles_w) * RW;
+  const int tiles_w = a.Wo >> rws;
+  const int tiles_img = (a.Ho / RH) * tiles_w;
+  const int b = tl.bx / tiles_img;
+  const int tr = tl.bx - b * tiles_img;
+  const int oh0 = (tr / tiles_w) * RH, ow0 = (tr % tiles_w) << rws;
   const int n0 = tl.by * BN;
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   const char* zero = reinterpret_cast<const char*>(a.zero);
-  const T* x1 = reinterpret_cast<const T*>(a.x1);
-  const T* x2 = reinterpret_cast<const T*>(a.x2);
-  const T* wgt = reinterpret_cast<const T*>(a.w);
   const int pixb = b * a.Hs * a.Ws;
 
-  // A rows of this lane: stage pixel p -> (oy, ox) with input column ow0 + ox - 1.
-  int a_oy[AG], a_iw[AG], a_ls[AG];
+  // Per lane and A row j: source pixel index for each kh (-1 = padding) and the 16-byte slot
+  // it fills (source-side swizzle).
+  int a_pix[AG][3], a_ls[AG];
 #pragma unroll
   for (int j = 0; j < AG; ++j) {
     const int p = (wave * AG + j) * 8 + (lane >> 3);
-    a_ls[j] = (lane & 7) ^ ((p >> 1) & 7);
-    if (p < NPIX) {
-      a_oy[j] = p / RWP;
-      a_iw[j] = ow0 + (p - a_oy[j] * RWP) - 1;
-    } else {
-      a_oy[j] = -100000; a_iw[j] = -100000;
+    a_ls[j] = ((lane & 7) ^ ((p >> 1) & 7)) * VE;
+    const int oy = p / RWP, iw = ow0 + (p - oy * RWP) - 1;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh0 + oy + kh - 1;
+      int pix = -1;
+      if (p < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
+        pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
+      a_pix[j][kh] = pix;
     }
   }
-  const T* b_row[BG];
-  int b_ls[BG], b_kw[BG];
+  // B rows: weight row pointer (tap kw folded in) and slot.
+  const T* b_ptr[BG];
+  int b_ls[BG];
 #pragma unroll
   for (int j = 0; j < BG; ++j) {
     const int row = (wave * BG + j) * 8 + (lane >> 3);
-    b_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
-    b_kw[j] = row / BN;
+    b_ls[j] = ((lane & 7) ^ ((row >> 1) & 7)) * VE;
     const int n = n0 + row % BN;
-    b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
+    b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
+                          : nullptr;
   }
-  const int nchunk = a.Cin / BKE;
-  const int nst = nchunk * 3;
+  // LDS byte offsets of this lane's MFMA fragments (stage-relative).
+  const int lr = lane & 15, lg = lane >> 4;
+  auto swz = [](int row, int sl) { return row * 128 + ((sl ^ ((row >> 1) & 7)) << 4); };
+  int aoff[TM][3][KSTEPS], boff[3][TN][KSTEPS];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WTM + i * 16 + lr;
+    const int oy = r >> rws;
+    const int p = oy * RWP + (r - (oy << rws));
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) aoff[i][kw][ks] = swz(p + kw, ks * 4 + lg);
+  }
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int jn = 0; jn < TN; ++jn)
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks)
+        boff[kw][jn][ks] = AROWS * 128 + swz(kw * BN + wn * WTN + jn * 16 + lr, ks * 4 + lg);
 
-  auto issue = [&](int s) {
-    char* st = smem + (s & 1) * STAGE;
-    const int c = s / 3, kh = s - c * 3;
+  const int nchunk = a.Cin / BKE;
+  auto issue = [&](int c, int kh, int buf) {
+    char* st = smem + buf * STAGE;
     const int ci0 = c * BKE;
     const bool from1 = ci0 < a.C1;
-    const T* xs = from1 ? x1 : x2;
-    const int ld = from1 ? a.ld1 : a.ld2;
-    const int cb = from1 ? ci0 : ci0 - a.C1;
+    const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) +
+                     (size_t)(from1 ? ci0 : ci0 - a.C1) * ES;
+    const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * ES;
 #pragma unroll
     for (int j = 0; j < AG; ++j) {
-      const int ih = oh0 + a_oy[j] + kh - 1, iw = a_iw[j];
-      const char* src = zero;
-      if ((unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win) {
-        const int sh = a.up ? (ih >> 1) : ih, sw = a.up ? (iw >> 1) : iw;
-        src = reinterpret_cast<const char*>(xs + (size_t)(pixb + sh * a.Ws + sw) * ld + cb +
-                                            a_ls[j] * VE);
-      }
+      const int pix = a_pix[j][kh];
+      const char* src = pix >= 0 ? xs + (size_t)pix * ldb + a_ls[j] * ES : zero;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                        (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < BG; ++j) {
-      const char* src = zero;
-      if (b_row[j])
-        src = reinterpret_cast<const char*>(b_row[j] + (kh * 3 + b_kw[j]) * a.Cin + ci0 + b_ls[j] * VE);
+      const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + kh * 3 * a.Cin + ci0 + b_ls[j])
+                                 : zero;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                        (lds_void_t*)(st + AROWS * 128 + (wave * BG + j) * 8 * 128),
                                        16, 0, 0);
     }
   };
-  auto swz = [](int row, int s) { return row * 128 + ((s ^ ((row >> 1) & 7)) << 4); };
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -440,51 +461,52 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int lr = lane & 15, lg = lane >> 4;
-  // Stage pixel of this lane's A fragment rows (tap kw = 0).
-  int a_pix[TM];
+  auto compute = [&](int buf) {
+    const char* st = smem + buf * STAGE;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int r = wm * WTM + i * 16 + lr;
-    const int oy = r / RW;
-    a_pix[i] = oy * RWP + (r - oy * RW);
-  }
-  issue(0);
-  for (int s = 0; s < nst; ++s) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (s + 1 < nst) issue(s + 1);               // refills the stage read at step s-1
-    const char* A = smem + (s & 1) * STAGE;
-    const char* Bs = A + AROWS * 128;
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
+    for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks) {
         u32x4 fa[TM], fb[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const u32x4*>(A + swz(a_pix[i] + kw, ks * 4 + lg));
+        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const u32x4*>(st + aoff[i][kw][ks]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const u32x4*>(Bs + swz(kw * BN + wn * WTN + j * 16 + lr, ks * 4 + lg));
+        for (int jn = 0; jn < TN; ++jn) fb[jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+          for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i], fb[jn]);
       }
-    }
+  };
+  auto sync_stage = [&]() {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // Stages s = 3c + kh alternate buffers; kh is unrolled so the A source table index is static.
+  issue(0, 0, 0);
+  int buf = 0;
+  for (int c = 0; c < nchunk; ++c) {
+    sync_stage();
+    issue(c, 1, buf ^ 1);
+    compute(buf);
+    buf ^= 1;
+    sync_stage();
+    issue(c, 2, buf ^ 1);
+    compute(buf);
+    buf ^= 1;
+    sync_stage();
+    if (c + 1 < nchunk) issue(c + 1, 0, buf ^ 1);
+    compute(buf);
+    buf ^= 1;
   }
   struct Rows {
-    int base, RW, Wo;
-    DEV int operator()(int t) const {
-      const int oy = t / RW;
-      return base + oy * Wo + (t - oy * RW);
-    }
+    int base, rws, Wo;
+    DEV int operator()(int t) const { return base + (t >> rws) * Wo + (t & ((1 << rws) - 1)); }
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const Rows rm{b * HWo + oh0 * a.Wo + ow0, RW, a.Wo};
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo);
+  const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
+  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b);
 }
 
 template <typename T, int KH, int KW, int S, int P>

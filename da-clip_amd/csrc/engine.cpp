@@ -869,8 +869,10 @@ class EngineT : public Engine {
     need(sched.T > 0, "schedule not set");
     need(t >= 1 && t <= sched.T, "t out of range");
     need(z != nullptr, "posterior_step needs explicit noise");
-    // eps is NCHW here (ld = 0 selects flat indexing in the kernel).
-    sde_step<float>(mode, x, mu, eps, 0, 1, 1, z, nullptr, 0, sched.coef(t, mode), 1, 1, n, st);
+    need(n > 0 && n % 3 == 0, "posterior_step: n must be B*3*H*W");
+    // eps is NCHW here (ld = 0 selects flat indexing in the kernel); the kernel covers
+    // B*3*H*W elements, so the flat view is B = H = 1, W = n / 3.
+    sde_step<float>(mode, x, mu, eps, 0, 1, 1, z, nullptr, 0, sched.coef(t, mode), 1, 1, n / 3, st);
     HIP_OK(hipGetLastError());
   }
 
@@ -922,7 +924,11 @@ class EngineT : public Engine {
     HIP_OK(hipStreamSynchronize(priv));       // seed_host staging is pageable
     // tc == nullptr is a different program (no prompt embedding): key it via mode bit.
     const int mkey = mode | (tc ? 0 : 2);
-    if (prof.kernel_id >= 0) {
+    static const bool no_graph = getenv("DAC_NO_GRAPH") && getenv("DAC_NO_GRAPH")[0] == '1';
+    if (no_graph && prof.kernel_id < 0) {
+      Run r = live(priv);
+      record_loop(r, b, mode, B, H, W, nT, noise);
+    } else if (prof.kernel_id >= 0) {
       // Profiling replay: HIP cannot report elapsed time between events recorded by graph
       // nodes (hipEventElapsedTime -> invalid handle), so the same launch sequence runs
       // eagerly on the same stream with an event pair around every launch of the class.
@@ -970,6 +976,8 @@ class EngineT : public Engine {
     HIP_OK(hipEventRecord(ev_out, priv));
     HIP_OK(hipStreamWaitEvent(st, ev_out, 0));
   }
+
+  void invalidate_graphs() override { clear_graphs(); }
 
   double unet_flops(int B, int H, int W) override {
     Arena a;

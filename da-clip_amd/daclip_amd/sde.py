@@ -141,6 +141,9 @@ class IRSDE:
             h = _lib.Handle(dev, "fp32", _lib.DacConfig())
             self._step_handle = h
         self._sync_schedule(h)
+        for name, v in (("eps", eps), ("mu", mu), ("z", z)):
+            if v.numel() != x.numel():
+                raise RuntimeError(f"step: {name} has {v.numel()} elements, x has {x.numel()}")
         out = x.contiguous().clone()
         with torch.cuda.device(dev):
             h.check(_lib.lib().dac_posterior_step(h.h, mode, _lib._ptr(out), _lib._ptr(eps.contiguous()),

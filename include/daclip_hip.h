@@ -105,7 +105,8 @@ int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu,
                     const float* text_ctx, const float* image_ctx, int B, int H, int W, int T,
                     const float* noise, uint64_t seed, void* stream);
 
-/* One sampler update given the model output: x <- step(x, eps, t, z) (z: [B,3,H,W]). */
+/* One sampler update given the model output: x <- step(x, eps, t, z); x, eps, mu, z are
+ * [B,3,H,W] fp32 and n = B*3*H*W elements (must be a multiple of 3). */
 int dac_posterior_step(dac_handle* h, int mode, float* x_inout, const float* eps,
                        const float* mu, const float* z, int t, int n, void* stream);
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include "../da-clip_amd/csrc/kernels.h"
 
@@ -14,6 +15,7 @@ struct Shape { const char* name; int B, H, W, cin, cout, kh, s, p, up, act, ss, 
 
 int main(int argc, char** argv) {
   int iters = argc > 1 ? atoi(argv[1]) : 20;
+  const char* only = argc > 2 ? argv[2] : nullptr;   // substring filter on the shape name
   std::vector<Shape> shapes = {
     {"L0 3x3 64->64 plain", 8, 256, 256, 64, 64, 3, 1, 1, 0, 0, 0, 0},
     {"L0 3x3 64->64 ss+silu", 8, 256, 256, 64, 64, 3, 1, 1, 0, 1, 1, 0},
@@ -35,6 +37,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(ss, 0, 8 * 8192 * 4)); CK(hipMemset(res, 0, maxe * 2));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto& s : shapes) {
+    if (only && !strstr(s.name, only)) continue;
     ConvArgs a{};
     a.x1 = x; a.ld1 = s.cin; a.C1 = s.cin; a.Cin = s.cin; a.Hs = s.H; a.Ws = s.W; a.up = s.up;
     a.B = s.B; a.Ho = (s.H + 2 * s.p - s.kh) / s.s + 1; a.Wo = (s.W + 2 * s.p - s.kh) / s.s + 1;
