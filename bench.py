@@ -52,26 +52,6 @@ def setup_dist(args):
     return ws, rank, local
 
 
-def broadcast_state(sd, keys, ws, rank, dev):
-    """Rank 0 owns the weights; one flat fp32 RCCL broadcast replicates them."""
-    shapes = [tuple(sd[k].shape) if rank == 0 else None for k in keys]
-    if ws > 1:
-        obj = [shapes]
-        dist.broadcast_object_list(obj, src=0)
-        shapes = obj[0]
-    sizes = [int(np.prod(s)) for s in shapes]
-    flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
-    if rank == 0:
-        flat.copy_(torch.from_numpy(np.concatenate([np.asarray(sd[k], np.float32).ravel() for k in keys])))
-    if ws > 1:
-        dist.broadcast(flat, src=0)
-    out, o = {}, 0
-    for k, s, n in zip(keys, shapes, sizes):
-        out[k] = flat[o:o + n].view(s)
-        o += n
-    return out
-
-
 def cpu_baseline(args, sd_unet, sd_clip):
     """Oracle (numpy fp32 restatement of the reference path) on the host cores: DaCLIP encode
     of one 224^2 image + `cpu_steps` of the 100 UNet+posterior steps at 256^2, B=1; the
@@ -106,7 +86,7 @@ def main():
     args = parse()
     ws, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
-    from daclip_amd import arch, synth, _lib
+    from daclip_amd import arch, synth, _lib, shard
     from daclip_amd.unet import ConditionalUNet
     from daclip_amd.open_clip import DaCLIP
     from daclip_amd.sde import IRSDE
@@ -116,8 +96,8 @@ def main():
     cspec = {k: s for k, s in arch.daclip_state_spec().items() if k.startswith(("clip.visual.", "visual_control."))}
     sd_u = synth.synth_state_dict(uspec, 0) if rank == 0 else None
     sd_c = synth.synth_state_dict(cspec, 0) if rank == 0 else None
-    wu = broadcast_state(sd_u, list(uspec), ws, rank, dev)
-    wc = broadcast_state(sd_c, list(cspec), ws, rank, dev)
+    wu = shard.broadcast_state(sd_u, list(uspec), dev)
+    wc = shard.broadcast_state(sd_c, list(cspec), dev)
 
     unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype=args.dtype)
     unet.load_state_dict(wu)
@@ -127,18 +107,25 @@ def main():
     sde = IRSDE(max_sigma=50, T=args.T, schedule="cosine", eps=0.005)
     sde.set_model(unet)
 
-    B, R = args.batch, args.res
-    lq = torch.from_numpy(synth.synth_images(B, R, R, seed=100 + rank * B)).to(dev)
-    img4clip = torch.from_numpy(synth.synth_noise((B, 3, 224, 224), seed=200 + rank, tag="clip")).to(dev)
+    # Weak scaling: the global batch is ws * batch images, rank r restores its contiguous
+    # shard (shard_bounds); inputs are keyed by global image index, and so is the device
+    # noise (image_offset), so every image restores identically for any world size.
+    R = args.res
+    n_glob = ws * args.batch
+    lo, hi = shard.shard_bounds(n_glob, ws, rank)
+    B = hi - lo
+    lq = torch.from_numpy(np.concatenate([synth.synth_images(1, R, R, seed=100 + g) for g in range(lo, hi)])).to(dev)
+    img4clip = torch.from_numpy(np.concatenate([synth.synth_noise((1, 3, 224, 224), seed=200 + g, tag="clip")
+                                                for g in range(lo, hi)])).to(dev)
     sde.set_mu(lq)
-    gather = [torch.empty_like(lq) for _ in range(ws)] if ws > 1 else None
+    sde.image_offset = lo
 
     def step():
         ic, dc = clip.encode_image(img4clip, control=True)
         noisy = sde.noise_state(lq)
         out = sde.reverse_posterior(noisy, text_context=dc, image_context=ic)
         if ws > 1:
-            dist.all_gather(gather, out)
+            out = shard.gather_outputs(out, n_glob)
         return out
 
     h = unet._h
@@ -179,7 +166,7 @@ def main():
     h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
 
     if rank == 0:
-        images = ws * B * args.steps
+        images = n_glob * args.steps
         ach = fl.value / (mean_ms.value * 1e-3) / 1e12 if n_launch > 0 else None
         roof = None
         if n_launch > 0:
@@ -201,7 +188,7 @@ def main():
                "data": "synthetic (random-init ViT-B/32 DA-CLIP + nf=64 ConditionalUNet, synthetic LQ)",
                "config": {"workload": f"deraining-shaped synthetic batch, {R}x{R}, batch={B}/GPU, "
                                       f"{args.T} IR-SDE posterior steps, hipGraph loop (BASELINE configs[1])",
-                          "batch_per_gpu": B, "global_batch": ws * B, "resolution": R, "sde_steps": args.T,
+                          "batch_per_gpu": B, "global_batch": n_glob, "resolution": R, "sde_steps": args.T,
                           "sampler": "posterior", "parallelism": f"dp{ws}"},
                "model_tflop_per_image": round(total_tf, 3),
                "whole_path_tflops": round(total_tf * images / el, 1),

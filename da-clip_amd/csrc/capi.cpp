@@ -202,6 +202,13 @@ int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu, co
   });
 }
 
+int dac_set_noise_offset(dac_handle* h, uint64_t first_image) {
+  return guard(h, [&]() -> int {
+    h->eng->set_noise_offset(first_image);
+    return DAC_OK;
+  });
+}
+
 int dac_posterior_step(dac_handle* h, int mode, float* x_inout, const float* eps, const float* mu,
                        const float* z, int t, int n, void* stream) {
   return guard(h, [&]() -> int {

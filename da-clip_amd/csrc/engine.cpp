@@ -806,7 +806,7 @@ class EngineT : public Engine {
     b.sin = dalloc<float>((size_t)nT * B * unet->nf);
     b.ldo = 4;
     b.out = dalloc<char>((size_t)B * Hp * Wp * b.ldo * sizeof(T));
-    b.seed = dalloc<uint64_t>(1);
+    b.seed = dalloc<uint64_t>(2);     // [seed, element offset of image 0]
     return bufs.emplace(key, b).first->second;
   }
   size_t plan_unet(int B, int H, int W, int nT) {
@@ -919,8 +919,9 @@ class EngineT : public Engine {
     HIP_OK(hipMemcpyAsync(b.mus, mu, n * 4, hipMemcpyDeviceToDevice, priv));
     if (tc) HIP_OK(hipMemcpyAsync(b.tcs, tc, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
     if (icx) HIP_OK(hipMemcpyAsync(b.ics, icx, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
-    seed_host = seed;
-    HIP_OK(hipMemcpyAsync(b.seed, &seed_host, 8, hipMemcpyHostToDevice, priv));
+    seed_host[0] = seed;
+    seed_host[1] = noise_offset * (uint64_t)(3 * H * W);
+    HIP_OK(hipMemcpyAsync(b.seed, seed_host, 16, hipMemcpyHostToDevice, priv));
     HIP_OK(hipStreamSynchronize(priv));       // seed_host staging is pageable
     // tc == nullptr is a different program (no prompt embedding): key it via mode bit.
     const int mkey = mode | (tc ? 0 : 2);
@@ -978,6 +979,7 @@ class EngineT : public Engine {
   }
 
   void invalidate_graphs() override { clear_graphs(); }
+  void set_noise_offset(uint64_t first_image) override { noise_offset = first_image; }
 
   double unet_flops(int B, int H, int W) override {
     Arena a;
@@ -1009,7 +1011,8 @@ class EngineT : public Engine {
   Arena arena;
   hipStream_t priv;
   hipEvent_t ev_in, ev_out;
-  uint64_t seed_host = 0;
+  uint64_t seed_host[2] = {0, 0};
+  uint64_t noise_offset = 0;     // global index of image 0 (sharded runs)
   void* zero_page = nullptr;
 };
 

@@ -136,6 +136,7 @@ class Engine {
   virtual void posterior_step(int mode, float* x, const float* eps, const float* mu,
                               const float* z, int t, int n, hipStream_t st) = 0;
   virtual double unet_flops(int B, int H, int W) = 0;
+  virtual void set_noise_offset(uint64_t first_image) = 0;
   virtual void invalidate_graphs() {}     // captured loops bake in the schedule
   virtual double encode_flops(int B) = 0;
   SdeSchedule sched;

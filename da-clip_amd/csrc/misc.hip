@@ -195,7 +195,7 @@ __global__ void sde_step_kernel(int mode, float* x, const float* mu, const T* ep
   const int b = (int)(i / ((size_t)W * H * 3));
   const float e = ld == 0 ? to_f(eps[i]) : to_f(eps[(((size_t)b * Hp + h) * Wp + w) * ld + ch]);
   const float xv = x[i], m = mu[i];
-  const float zv = z ? z[i] : philox_normal(*seedp, tag, i);
+  const float zv = z ? z[i] : philox_normal(seedp[0], tag, i + seedp[1]);
   float out;
   if (mode == 0) {
     const float x0 = ((xv - m) - c.sbar * e) * c.ea + m;                  // sde_utils.py:245-247

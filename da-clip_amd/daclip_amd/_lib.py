@@ -25,7 +25,7 @@ DAC_E_MISSING, DAC_E_KEY = -3, -2
 
 EXPORTS = ["dac_create", "dac_destroy", "dac_set_weight", "dac_finalize_weights",
            "dac_encode_image", "dac_unet_forward", "dac_sde_schedule", "dac_sde_reverse",
-           "dac_posterior_step", "dac_unet_flops", "dac_encode_flops", "dac_profile_enable",
+           "dac_set_noise_offset", "dac_posterior_step", "dac_unet_flops", "dac_encode_flops", "dac_profile_enable",
            "dac_profile_read", "dac_last_error"]
 
 
@@ -60,6 +60,7 @@ def lib() -> ctypes.CDLL:
         "dac_unet_forward": (I, [P, P, P, F, P, P, I, I, I, P, P]),
         "dac_sde_schedule": (I, [P, F, I, I, F, P, F]),
         "dac_sde_reverse": (I, [P, I, P, P, P, P, I, I, I, I, P, U64, P]),
+        "dac_set_noise_offset": (I, [P, U64]),
         "dac_posterior_step": (I, [P, I, P, P, P, P, I, I, P]),
         "dac_unet_flops": (D, [P, I, I, I]),
         "dac_encode_flops": (D, [P, I]),

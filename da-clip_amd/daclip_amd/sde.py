@@ -32,6 +32,9 @@ class IRSDE:
         self.eps = eps
         self._initialize(self.max_sigma, self.sample_T, schedule, eps)
         self.seed = 0
+        # Global index of image 0 of the batch this process restores (sharded runs): the
+        # device noise of image b is keyed by image_offset + b (dac_set_noise_offset).
+        self.image_offset = 0
 
     def _initialize(self, max_sigma, T, schedule, eps=0.01):
         # Verbatim torch op sequence of sde_utils.py:112-151 (fp32 CPU).
@@ -120,6 +123,7 @@ class IRSDE:
             with torch.cuda.device(dev):
                 self._sync_schedule(h)
                 self.seed += 1
+                h.check(_lib.lib().dac_set_noise_offset(h.h, int(self.image_offset)), "noise_offset")
                 h.check(_lib.lib().dac_sde_reverse(h.h, mode, _lib._ptr(x), _lib._ptr(mu_d),
                                                    _lib._ptr(tc), _lib._ptr(ic), B, H, W, int(T),
                                                    _lib._ptr(nz), self.seed, h.stream()),

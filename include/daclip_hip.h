@@ -105,6 +105,12 @@ int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu,
                     const float* text_ctx, const float* image_ctx, int B, int H, int W, int T,
                     const float* noise, uint64_t seed, void* stream);
 
+/* Device-noise keying for sharded runs: with noise == NULL, element e of image b draws
+ * Philox(seed, step, (first_image + b) * 3*H*W + e), so a shard whose first global image is
+ * `first_image` reproduces exactly the noise that image receives in an unsharded batch
+ * (results are independent of the world size). Default 0. */
+int dac_set_noise_offset(dac_handle* h, uint64_t first_image);
+
 /* One sampler update given the model output: x <- step(x, eps, t, z); x, eps, mu, z are
  * [B,3,H,W] fp32 and n = B*3*H*W elements (must be a multiple of 3). */
 int dac_posterior_step(dac_handle* h, int mode, float* x_inout, const float* eps,

@@ -3,8 +3,9 @@
 set -o pipefail
 TAG=${1:-r}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_hip_parity.py -x -v --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/test_$TAG.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/test_$TAG.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/test_$TAG.log; exit 1; }
 tail -3 gpurun_out/test_$TAG.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/smoke_$TAG.log; exit 1; }
 timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > gpurun_out/bench_$TAG.log 2>&1 || { echo BENCH FAILED; tail -20 gpurun_out/bench_$TAG.log; exit 1; }
 grep '^{' gpurun_out/bench_$TAG.log
 export TMPDIR=/tmp
