@@ -24,6 +24,24 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "restored images/sec @256x256, 100 IR-SDE steps; PSNR vs ref; 1/2/4/8 MI355X"
 MFMA_PEAK = {"bf16": 2500.0, "fp32": 157.3}       # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                                  # GB/s
+# Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
+# PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
+KERNEL_SYMBOL = {
+    (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi256ELi64ELi4ELi2EEEvNS_8ConvArgsEi",
+    (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi4EEEvNS_8ConvArgsEi",
+    (306, "fp32"): "_ZN3dac12conv3_kernelIfLi256ELi64ELi4ELi2EEEvNS_8ConvArgsEi",
+    (307, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi4EEEvNS_8ConvArgsEi",
+}
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_entry(kernel_id, dtype):
+    """Per-dispatch PMC figures of the timed kernel (same bench workload), or None."""
+    sym = KERNEL_SYMBOL.get((kernel_id, dtype))
+    if sym is None or not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as f:
+        return json.load(f)["kernels"].get(sym)
 
 
 def parse():
@@ -38,6 +56,7 @@ def parse():
     p.add_argument("--kernel-id", type=int, default=306,
                    help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo 256x64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")
     return p.parse_args()
 
@@ -149,31 +168,40 @@ def main():
         el = float(t.item())
 
     finite = bool(torch.isfinite(out).all().item())
-    # Roofline of the dominant kernel: one more restore of the same batch on the same stream,
-    # replayed eagerly with HIP events around every launch of the timed conv class (HIP
-    # cannot time events recorded inside graph replays).
-    h.check(_lib.lib().dac_profile_enable(h.h, args.kernel_id), "profile_enable")
-    torch.cuda.synchronize()
-    tp = time.perf_counter()
-    step()
-    torch.cuda.synchronize()
-    eager_ms = (time.perf_counter() - tp) * 1e3
+    n_launch = 0
     mean_ms = _lib.ctypes.c_double()
     fl = _lib.ctypes.c_double()
     by = _lib.ctypes.c_double()
-    n_launch = h.check(_lib.lib().dac_profile_read(h.h, _lib.ctypes.byref(mean_ms), _lib.ctypes.byref(fl),
-                                                   _lib.ctypes.byref(by)), "profile_read")
-    h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
+    eager_ms = 0.0
+    if not args.no_roofline:
+        # Roofline of the dominant kernel: one more restore of the same batch on the same stream,
+        # replayed eagerly with HIP events around every launch of the timed conv class (HIP
+        # cannot time events recorded inside graph replays).
+        h.check(_lib.lib().dac_profile_enable(h.h, args.kernel_id), "profile_enable")
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - tp) * 1e3
+        n_launch = h.check(_lib.lib().dac_profile_read(h.h, _lib.ctypes.byref(mean_ms), _lib.ctypes.byref(fl),
+                                                       _lib.ctypes.byref(by)), "profile_read")
+        h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
 
     if rank == 0:
         images = n_glob * args.steps
         ach = fl.value / (mean_ms.value * 1e-3) / 1e12 if n_launch > 0 else None
         roof = None
+        pmc = pmc_entry(args.kernel_id, args.dtype)
         if n_launch > 0:
             roof = {"kernel": f"conv_kernel class {args.kernel_id} (3x3 implicit-GEMM, {args.dtype})",
                     "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_PEAK[args.dtype],
                     "unit": "TFLOP/s", "frac": round(ach / MFMA_PEAK[args.dtype], 4),
-                    "traffic": None, "launches_timed": n_launch,
+                    "traffic": pmc["hbm_bytes_per_dispatch"] if pmc else None,
+                    "traffic_source": ("profiles/pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (KiB->B, gfx950 "
+                                       "x2 read correction) per dispatch of this kernel, rocprofv3 --pmc over "
+                                       "this bench command") if pmc else None,
+                    "mfma_busy_pmc": round(pmc["mfma_busy"], 4) if pmc and "mfma_busy" in pmc else None,
+                    "launches_timed": n_launch,
                     "mean_launch_us": round(mean_ms.value * 1e3, 2),
                     "flops_per_launch": fl.value, "algorithmic_bytes_per_launch": by.value,
                     "achieved_hbm_GBps": round(by.value / (mean_ms.value * 1e-3) / 1e9, 1),
