@@ -27,10 +27,10 @@ HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
-    (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi256ELi64ELi4ELi2EEEvNS_8ConvArgsEi",
-    (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi4EEEvNS_8ConvArgsEi",
-    (306, "fp32"): "_ZN3dac12conv3_kernelIfLi256ELi64ELi4ELi2EEEvNS_8ConvArgsEi",
-    (307, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi4EEEvNS_8ConvArgsEi",
+    (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
+    (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
+    (306, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
+    (307, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
 }
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--T", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--kernel-id", type=int, default=306,
-                   help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo 256x64)")
+                   help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo, Cout<=64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")

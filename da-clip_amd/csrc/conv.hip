@@ -10,7 +10,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 
 // Kernel variant conv_dispatch selects (mirrors its logic); used to label timed launches:
 // 0/1/2 = v1 256x16 / 256x64 / 128x128, 3/4/5 = v2 256x64 / 256x128 / 128x128,
-// 6/7 = v3 (row-halo 3x3) 256x64 / 128x128.
+// 6/7 = v3 (row-halo 3x3, 64-byte rows, 4 waves) 128x64 / 128x128, 10/11 = v3 (128-byte rows,
+// 8 waves) 256x64 / 128x128, 8 = v2 single-stage 1x1 (K = one tile) 128x64.
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -26,10 +27,12 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   const int gz = batched ? a.B : 1;
   const bool v2ok = V2 && a.zero && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
   if (kh == 3 && v2ok && !batched && conv3_rw_host(a, 256) > 0) {
-    if (a.Cout <= 64) return 6;
-    if (conv3_rw_host(a, 128) > 0) return 7;
+    if (a.Cout <= 64) return conv3_rw_host(a, 128) > 0 ? 6 : 10;
+    if (conv3_rw_host(a, 128) > 0)
+      return (long)(a.B * a.Ho * a.Wo / 128) * ((a.Cout + 127) / 128) >= 512 ? 7 : 11;
   }
   if (v2ok) {
+    if (kh == 1 && a.K <= BKE) return 8;
     if (a.Cout <= 64) return 3;
     if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) return 4;
     return 5;

@@ -8,6 +8,9 @@
 // + res1 + res2 + per-image bias, one 16-byte store; rows map through `rowmap` (row-halo
 // tiles are 2-D in the image). Partial / misaligned chunks fall back to scalars.
 // Keeping the LDS image in fp32 keeps the residual adds in fp32 like the reference.
+// The tile goes through LDS in BM / EPR passes of EPR rows (EPR a multiple of the wave row
+// height), so the epilogue never needs more LDS than the main loop's pipeline: the kernels
+// pick EPR to keep several blocks resident per CU.
 #pragma once
 #include "common.h"
 #include "kernels.h"
@@ -29,10 +32,21 @@ struct EpiLds {
   static constexpr int BYTES = BM * LDW * 4;
 };
 
-template <typename T, int BM, int BN, int WGM, int WGN, class RowMap>
-DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
+// Largest pass height (multiple of WTM dividing BM) whose fp32 tile fits in `budget` bytes;
+// WTM if none does (the caller then sizes LDS for that).
+template <int BM, int BN, int WTM>
+constexpr int epi_rows(int budget) {
+  int best = WTM;
+  for (int r = WTM; r <= BM; r += WTM)
+    if (BM % r == 0 && EpiLds<1, BN>::LDW * 4 * r <= budget) best = r;
+  return best;
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN, int EPR, class RowMap>
+DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
                            char* smem, int M, const RowMap& rowmap, int n0, int HWo, int bimg) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
+  static_assert(EPR % WTM == 0 && BM % EPR == 0, "epilogue pass height");
   constexpr int NT = 64 * WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int LDW = EpiLds<BM, BN>::LDW;
@@ -40,86 +54,34 @@ DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][
   const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
   const bool geglu = a.act == ACT_GEGLU;
+  const bool fast = !geglu && bimg >= 0;
   float* tile = reinterpret_cast<float*>(smem);
-  __syncthreads();                                   // main-loop LDS reads are finished
 
-  if (!geglu && bimg >= 0) {
-    // Fast path: all rows of the tile belong to image bimg -> per-channel terms in registers.
-    float sc[TN], sh[TN], bi[TN];
+  // Fast path: all rows of the tile belong to image bimg -> per-channel terms in registers.
+  float sc[TN], sh[TN], bi[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
+  for (int j = 0; j < TN; ++j) {
+    sc[j] = 1.f; sh[j] = 0.f; bi[j] = 0.f;
+    if (fast) {
       const int n = n0 + wn * WTN + j * 16 + lr;
       const bool ok = n < a.Cout;
       bi[j] = (a.bias && ok) ? a.bias[n] : 0.f;
-      sc[j] = 1.f; sh[j] = 0.f;
       if (a.ss && ok) {
         const float* s = a.ss + (size_t)bimg * a.ss_ld;
         sc[j] = s[n] + 1.f;
         sh[j] = s[a.Cout + n];
       }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float* row = tile + (wm * WTM + i * 16 + lg * 4 + r) * LDW + wn * WTN + lr;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float v = (acc[i][j][r] + bi[j]) * sc[j] + sh[j];
-          if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if (a.act == ACT_GELU) v = gelu_f(v);
-          row[j * 16] = v;
-        }
-      }
-  } else {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = wm * WTM + i * 16 + lg * 4 + r;
-        const int m = rowmap(t);
-        const int b = bimg >= 0 ? bimg : (m < M ? m / HWo : 0);
-        float* row = tile + t * LDW;
-        if (geglu) {
-          if constexpr (TN % 2 == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; j += 2) {
-              const int cx = wn * WTN + j * 16 + lr;
-              const int nx = n0 + cx;
-              float vx = acc[i][j][r], vg = acc[i][j + 1][r];
-              if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
-              row[(wn * WTN + j * 16) / 2 + lr] = vx * gelu_f(vg);
-            }
-          }
-          continue;
-        }
-        const float* s = a.ss ? a.ss + (size_t)b * a.ss_ld : nullptr;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int c = wn * WTN + j * 16 + lr;
-          const int n = n0 + c;
-          float v = acc[i][j][r];
-          if (n < a.Cout) {
-            if (a.bias) v += a.bias[n];
-            if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
-          }
-          if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if (a.act == ACT_GELU) v = gelu_f(v);
-          row[c] = v;
-        }
-      }
-    }
   }
-  __syncthreads();
 
   T* y = reinterpret_cast<T*>(a.y);
   const T* r1 = reinterpret_cast<const T*>(a.res1);
   const T* r2 = reinterpret_cast<const T*>(a.res2);
   const bool vec_ok = (a.ldy % VE == 0) && (!r1 || a.ldr1 % VE == 0) && (!r2 || a.ldr2 % VE == 0);
-  auto emit = [&](int t, int cc, int n, int Cout) {
+  // t: tile row, src: its LDS row.
+  auto emit = [&](int t, const float* src, int n, int Cout) __attribute__((always_inline)) {
     const int m = rowmap(t);
     if (m >= M || n >= Cout) return;
-    const float* src = tile + t * LDW + cc;
     float v[VE];
 #pragma unroll
     for (int e = 0; e < VE; e += 4) {
@@ -155,22 +117,90 @@ DEV void conv_epilogue_lds(const ConvArgs& a, const f32x4 (&acc)[BM / WGM / 16][
       }
     }
   };
-  if (!geglu) {
-    constexpr int CPR = BN / VE;                     // 16-byte chunks per tile row
+
+  // Phase 1a, once: bias -> scale/shift -> activation (GEGLU: x * gelu(gate) into the even
+  // tile) in place on the accumulators. Doing it before the pass loop keeps the (speculated)
+  // math out of the per-pass guarded stores.
+  if (fast) {
 #pragma unroll
-    for (int k = 0; k < BM * CPR / NT; ++k) {
-      const int c = tid + k * NT;
-      const int t = c / CPR, cc = (c % CPR) * VE;
-      emit(t, cc, n0 + cc, a.Cout);
-    }
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v = (acc[i][j][r] + bi[j]) * sc[j] + sh[j];
+          if (a.act == ACT_SILU) v = silu_t<T>(v);
+          else if (a.act == ACT_GELU) v = gelu_f(v);
+          acc[i][j][r] = v;
+        }
   } else {
-    constexpr int CPR = BN / 2 / VE;
 #pragma unroll
-    for (int k = 0; k < (BM * CPR + NT - 1) / NT; ++k) {
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = wm * WTM + i * 16 + lg * 4 + r;
+        if (geglu) {
+          if constexpr (TN % 2 == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; j += 2) {
+              const int nx = n0 + wn * WTN + j * 16 + lr;
+              float vx = acc[i][j][r], vg = acc[i][j + 1][r];
+              if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
+              acc[i][j][r] = vx * gelu_f(vg);
+            }
+          }
+          continue;
+        }
+        const int m = rowmap(t);
+        const int b = bimg >= 0 ? bimg : (m < M ? m / HWo : 0);
+        const float* s = a.ss ? a.ss + (size_t)b * a.ss_ld : nullptr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * WTN + j * 16 + lr;
+          float v = acc[i][j][r];
+          if (n < a.Cout) {
+            if (a.bias) v += a.bias[n];
+            if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
+          }
+          if (a.act == ACT_SILU) v = silu_t<T>(v);
+          else if (a.act == ACT_GELU) v = gelu_f(v);
+          acc[i][j][r] = v;
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int r0 = 0; r0 < BM; r0 += EPR) {
+    __syncthreads();                                 // main-loop / previous-pass LDS reads done
+    // Phase 1b: the waves whose rows fall in this pass store them (fp32) to the LDS tile.
+    if (wm * WTM >= r0 && wm * WTM < r0 + EPR) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float* row = tile + (wm * WTM - r0 + i * 16 + lg * 4 + r) * LDW;
+          if (geglu) {
+            if constexpr (TN % 2 == 0) {
+#pragma unroll
+              for (int j = 0; j < TN; j += 2) row[(wn * WTN + j * 16) / 2 + lr] = acc[i][j][r];
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) row[wn * WTN + j * 16 + lr] = acc[i][j][r];
+          }
+        }
+    }
+    __syncthreads();
+    const int CPR = geglu ? BN / 2 / VE : BN / VE;   // 16-byte chunks per tile row
+    const int nch = EPR * CPR;
+#pragma unroll
+    for (int k = 0; k < (EPR * (BN / VE) + NT - 1) / NT; ++k) {
       const int c = tid + k * NT;
-      if (c >= BM * CPR) break;
-      const int t = c / CPR, cc = (c % CPR) * VE;
-      emit(t, cc, n0 / 2 + cc, a.Cout / 2);
+      if (c >= nch) break;
+      const int tl = c / CPR, cc = (c % CPR) * VE;
+      if (geglu) emit(r0 + tl, tile + tl * LDW + cc, n0 / 2 + cc, a.Cout / 2);
+      else emit(r0 + tl, tile + tl * LDW + cc, n0 + cc, a.Cout);
     }
   }
 }

@@ -47,8 +47,9 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
   constexpr int BV = (BN + 31) / 32;
   constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
   static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "tile");
-  constexpr int SMEM = 2 * (BM + BN) * 128 > EpiLds<BM, BN>::BYTES ? 2 * (BM + BN) * 128
-                                                                   : EpiLds<BM, BN>::BYTES;
+  constexpr int PIPE = 2 * (BM + BN) * 128;
+  constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
+  constexpr int SMEM = PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -182,7 +183,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 
@@ -208,7 +209,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
   constexpr int STAGE = (BM + BN) * 128;
   static_assert(AG >= 1 && BG >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
-  constexpr int SMEM = STAGES * STAGE > EpiLds<BM, BN>::BYTES ? STAGES * STAGE : EpiLds<BM, BN>::BYTES;
+  constexpr int PIPE = STAGES * STAGE;
+  constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
+  constexpr int SMEM = PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -294,13 +297,22 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   for (int s = 0; s < STAGES - 1; ++s) issue(s);
   const int lr = lane & 15, lg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    // Own DMA of tile kt done (STAGES-2 younger tiles may stay in flight), then barrier.
-    if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    else if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(AG + BG) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * (AG + BG)) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(kt + STAGES - 1);                      // refills the slot read at iteration kt-1
+    if constexpr (STAGES == 1) {
+      // Single buffer (K fits one tile, or LDS kept small for occupancy): fill, wait, use.
+      if (kt > 0) __syncthreads();               // everyone is done reading the buffer
+      issue(kt);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      // Own DMA of tile kt done (STAGES-2 younger tiles may stay in flight), then barrier.
+      if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(AG + BG) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * (AG + BG)) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue(kt + STAGES - 1);                    // refills the slot read at iteration kt-1
+    }
     const char* A = smem + (kt % STAGES) * STAGE;
     const char* Bs = A + BM * 128;
 #pragma unroll
@@ -321,7 +333,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 
@@ -346,22 +358,29 @@ inline int conv3_rw(const ConvArgs& a, int BM = 256) {
   return RW;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN>
+// CK = bytes of one LDS row (one K chunk of one pixel): 128 (8 slots) or 64 (4 slots). A
+// wave-instruction of global_load_lds fills 64 / SLOTS rows; slot swizzle sl ^ f(row) with
+// f(row) = (row >> log2(16 / SLOTS)) & (SLOTS - 1) keeps the 16 rows read by one ds_read_b128
+// lane group on distinct banks.
+template <typename T, int BM, int BN, int WGM, int WGN, int CK>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
-  constexpr int BKE = 128 / ES;
+  constexpr int BKE = CK / ES;
+  constexpr int SLOTS = CK / 16, RPI = 64 / SLOTS, SSH = SLOTS == 8 ? 1 : 2;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int NPIX_MAX = BM + 2 * (BM / 16);           // RH * (RW + 2) with RW >= 16
-  constexpr int AG = (NPIX_MAX + 8 * NW - 1) / (8 * NW);
-  constexpr int BG = 3 * BN / (8 * NW);
-  constexpr int AROWS = AG * 8 * NW;
-  constexpr int STAGE = (AROWS + 3 * BN) * 128;
+  constexpr int AG = (NPIX_MAX + RPI * NW - 1) / (RPI * NW);
+  constexpr int BG = 3 * BN / (RPI * NW);
+  constexpr int AROWS = AG * RPI * NW;
+  constexpr int STAGE = (AROWS + 3 * BN) * CK;
   constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
-  static_assert(BG >= 1 && (3 * BN) % (8 * NW) == 0, "tile");
-  constexpr int SMEM = 2 * STAGE > EpiLds<BM, BN>::BYTES ? 2 * STAGE : EpiLds<BM, BN>::BYTES;
+  static_assert(SLOTS == 8 || SLOTS == 4, "CK");
+  static_assert(BG >= 1 && (3 * BN) % (RPI * NW) == 0 && KSTEPS >= 1, "tile");
+  constexpr int EPR = epi_rows<BM, BN, WTM>(2 * STAGE);
+  constexpr int SMEM = 2 * STAGE > EpiLds<EPR, BN>::BYTES ? 2 * STAGE : EpiLds<EPR, BN>::BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -379,14 +398,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   const char* zero = reinterpret_cast<const char*>(a.zero);
   const int pixb = b * a.Hs * a.Ws;
+  auto fsw = [](int row) { return (row >> SSH) & (SLOTS - 1); };
 
   // Per lane and A row j: source pixel index for each kh (-1 = padding) and the 16-byte slot
   // it fills (source-side swizzle).
   int a_pix[AG][3], a_ls[AG];
 #pragma unroll
   for (int j = 0; j < AG; ++j) {
-    const int p = (wave * AG + j) * 8 + (lane >> 3);
-    a_ls[j] = ((lane & 7) ^ ((p >> 1) & 7)) * VE;
+    const int p = (wave * AG + j) * RPI + lane / SLOTS;
+    a_ls[j] = ((lane % SLOTS) ^ fsw(p)) * VE;
     const int oy = p / RWP, iw = ow0 + (p - oy * RWP) - 1;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
@@ -402,15 +422,15 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   int b_ls[BG];
 #pragma unroll
   for (int j = 0; j < BG; ++j) {
-    const int row = (wave * BG + j) * 8 + (lane >> 3);
-    b_ls[j] = ((lane & 7) ^ ((row >> 1) & 7)) * VE;
+    const int row = (wave * BG + j) * RPI + lane / SLOTS;
+    b_ls[j] = ((lane % SLOTS) ^ fsw(row)) * VE;
     const int n = n0 + row % BN;
     b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
                           : nullptr;
   }
   // LDS byte offsets of this lane's MFMA fragments (stage-relative).
   const int lr = lane & 15, lg = lane >> 4;
-  auto swz = [](int row, int sl) { return row * 128 + ((sl ^ ((row >> 1) & 7)) << 4); };
+  auto swz = [&](int row, int sl) { return row * CK + ((sl ^ fsw(row)) << 4); };
   int aoff[TM][3][KSTEPS], boff[3][TN][KSTEPS];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -428,7 +448,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
     for (int jn = 0; jn < TN; ++jn)
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks)
-        boff[kw][jn][ks] = AROWS * 128 + swz(kw * BN + wn * WTN + jn * 16 + lr, ks * 4 + lg);
+        boff[kw][jn][ks] = AROWS * CK + swz(kw * BN + wn * WTN + jn * 16 + lr, ks * 4 + lg);
 
   const int nchunk = a.Cin / BKE;
   auto issue = [&](int c, int kh, int buf) {
@@ -443,14 +463,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
       const int pix = a_pix[j][kh];
       const char* src = pix >= 0 ? xs + (size_t)pix * ldb + a_ls[j] * ES : zero;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                       (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
+                                       (lds_void_t*)(st + (wave * AG + j) * RPI * CK), 16, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < BG; ++j) {
       const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + kh * 3 * a.Cin + ci0 + b_ls[j])
                                  : zero;
       __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                       (lds_void_t*)(st + AROWS * 128 + (wave * BG + j) * 8 * 128),
+                                       (lds_void_t*)(st + AROWS * CK + (wave * BG + j) * RPI * CK),
                                        16, 0, 0);
     }
   };
@@ -506,7 +526,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
-  conv_epilogue_lds<T, BM, BN, WGM, WGN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b);
 }
 
 template <typename T, int KH, int KW, int S, int P>
@@ -523,19 +543,39 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     const int RW = conv3_rw(a);
     if (v2ok && RW > 0 && a.w_bstride == 0) {
+      // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
+      // blocks share a CU and one block's LDS-DMA latency hides behind another's MFMAs
+      // (measured 10-24 % faster than one 8-wave block with 128-byte rows). Small grids
+      // (< 2 blocks per CU, the 32x32 level) keep the 8-wave block.
+      if (a.Cout <= 64 && conv3_rw(a, 128) > 0) {
+        dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 63) / 64, 1);
+        conv3_kernel<T, 128, 64, 2, 2, 64><<<g, 256, 0, st>>>(a, conv3_rw(a, 128));
+        return;
+      }
       if (a.Cout <= 64) {
         dim3 g(a.B * a.Ho * a.Wo / 256, (a.Cout + 63) / 64, 1);
-        conv3_kernel<T, 256, 64, 4, 2><<<g, 512, 0, st>>>(a, RW);
+        conv3_kernel<T, 256, 64, 4, 2, 128><<<g, 512, 0, st>>>(a, RW);
         return;
       }
       if (conv3_rw(a, 128) > 0) {
         dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 127) / 128, 1);
-        conv3_kernel<T, 128, 128, 2, 4><<<g, 512, 0, st>>>(a, conv3_rw(a, 128));
+        if ((long)g.x * g.y >= 512)
+          conv3_kernel<T, 128, 128, 2, 2, 64><<<g, 256, 0, st>>>(a, conv3_rw(a, 128));
+        else
+          conv3_kernel<T, 128, 128, 2, 4, 128><<<g, 512, 0, st>>>(a, conv3_rw(a, 128));
         return;
       }
     }
   }
   if constexpr (V2) if (v2ok) {
+    if constexpr (KH == 1) if (a.K <= BKE) {
+      // One K tile (1x1 over 64 bf16 channels): no pipeline to fill, so a single small
+      // stage (128x64, 4 waves) keeps several blocks resident per CU and their load
+      // latencies overlap (measured best of 256x128 x {1,2,3} stages, 128x128, 128x64).
+      dim3 g((Mg + 127) / 128, (a.Cout + 63) / 64, gz);
+      conv2_kernel<T, 128, 64, 2, 2, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
+      return;
+    }
     if (a.Cout <= 64) {
       dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, gz);
       conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P><<<g, 512, 0, st>>>(a);

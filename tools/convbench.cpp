@@ -1,9 +1,12 @@
 // Standalone microbenchmark of the conv kernels (links da-clip_amd/build/conv*.o).
-// Usage: convbench [iters]   — prints per-shape time and TFLOP/s for bf16.
+// Usage: convbench [iters] [shape-substring] [check]
+//   prints per-shape time and TFLOP/s for bf16; with "check" the inputs are random and every
+//   output is compared with a naive reference conv (fp32 accumulate, same epilogue).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <vector>
 #include "../da-clip_amd/csrc/kernels.h"
 
@@ -13,9 +16,51 @@ typedef __bf16 bf16;
 
 struct Shape { const char* name; int B, H, W, cin, cout, kh, s, p, up, act, ss, res; };
 
+__global__ void fill_rand(bf16* p, size_t n, uint32_t seed, float scale) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+  h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+  p[i] = (bf16)(((h & 0xffff) / 65535.f - 0.5f) * scale);
+}
+__global__ void fill_rand_f(float* p, size_t n, uint32_t seed, float scale) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+  h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+  p[i] = ((h & 0xffff) / 65535.f - 0.5f) * scale;
+}
+// Naive reference: one thread per output element; weights [Cout][kh][kw][Cin].
+__global__ void ref_conv(ConvArgs a, int kh, int s, int p, float* out) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t M = (size_t)a.B * a.Ho * a.Wo;
+  if (i >= M * a.Cout) return;
+  const int n = i % a.Cout;
+  const size_t m = i / a.Cout;
+  const int b = m / (a.Ho * a.Wo), r = m % (a.Ho * a.Wo), oh = r / a.Wo, ow = r % a.Wo;
+  const bf16* x = (const bf16*)a.x1;
+  const bf16* w = (const bf16*)a.w;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  float acc = 0.f;
+  for (int y = 0; y < kh; ++y)
+    for (int z = 0; z < kh; ++z) {
+      const int ih = oh * s - p + y, iw = ow * s - p + z;
+      if (ih < 0 || iw < 0 || ih >= Hin || iw >= Win) continue;
+      const int sh = a.up ? ih >> 1 : ih, sw = a.up ? iw >> 1 : iw;
+      const bf16* xp = x + ((size_t)(b * a.Hs + sh) * a.Ws + sw) * a.ld1;
+      const bf16* wp = w + (((size_t)n * kh + y) * kh + z) * a.Cin;
+      for (int c = 0; c < a.Cin; ++c) acc += (float)xp[c] * (float)wp[c];
+    }
+  if (a.ss) acc = acc * (a.ss[(size_t)b * a.ss_ld + n] + 1.f) + a.ss[(size_t)b * a.ss_ld + a.Cout + n];
+  if (a.act == 1) acc = acc / (1.f + expf(-acc));
+  if (a.res1) acc += (float)((const bf16*)a.res1)[m * a.ldr1 + n];
+  out[i] = acc;
+}
+
 int main(int argc, char** argv) {
   int iters = argc > 1 ? atoi(argv[1]) : 20;
-  const char* only = argc > 2 ? argv[2] : nullptr;   // substring filter on the shape name
+  const char* only = argc > 2 && argv[2][0] ? argv[2] : nullptr;   // substring filter
+  const bool check = argc > 3 && !strcmp(argv[3], "check");
   std::vector<Shape> shapes = {
     {"L0 3x3 64->64 plain", 8, 256, 256, 64, 64, 3, 1, 1, 0, 0, 0, 0},
     {"L0 3x3 64->64 ss+silu", 8, 256, 256, 64, 64, 3, 1, 1, 0, 1, 1, 0},
@@ -26,6 +71,11 @@ int main(int argc, char** argv) {
     {"L3 3x3 512->512", 8, 32, 32, 512, 512, 3, 1, 1, 0, 1, 1, 0},
     {"L0 1x1 64->384", 8, 256, 256, 64, 384, 1, 1, 0, 0, 0, 0, 0},
     {"L0 1x1 128->64", 8, 256, 256, 128, 64, 1, 1, 0, 0, 0, 0, 0},
+    {"L1 1x1 64->384", 8, 128, 128, 64, 384, 1, 1, 0, 0, 0, 0, 0},
+    {"L1 1x1 128->384", 8, 128, 128, 128, 384, 1, 1, 0, 0, 0, 0, 0},
+    {"L2 1x1 256->384", 8, 64, 64, 256, 384, 1, 1, 0, 0, 0, 0, 0},
+    {"L1 3x3 64->64", 8, 128, 128, 64, 64, 3, 1, 1, 0, 1, 1, 0},
+    {"L1 3x3 128->128", 8, 128, 128, 128, 128, 3, 1, 1, 0, 1, 1, 0},
     {"L3 1x1 512->4096", 8, 32, 32, 512, 4096, 1, 1, 0, 0, 0, 0, 0},
   };
   size_t maxe = (size_t)8 * 256 * 256 * 512;
@@ -35,6 +85,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ss, 8 * 8192 * 4)); CK(hipMalloc(&bias, 8192 * 4));
   CK(hipMemset(zero, 0, 256)); CK(hipMemset(x, 0x3c, maxe * 2)); CK(hipMemset(w, 0x3c, (size_t)4096 * 9 * 1024 * 2));
   CK(hipMemset(ss, 0, 8 * 8192 * 4)); CK(hipMemset(res, 0, maxe * 2));
+  float* refo = nullptr;
+  bf16* yh = nullptr;
+  if (check) {
+    const size_t nw = (size_t)4096 * 9 * 1024;
+    fill_rand<<<(maxe + 255) / 256, 256>>>((bf16*)x, maxe, 1, 2.f);
+    fill_rand<<<(nw + 255) / 256, 256>>>((bf16*)w, nw, 2, 0.1f);
+    fill_rand<<<(maxe + 255) / 256, 256>>>((bf16*)res, maxe, 3, 2.f);
+    fill_rand_f<<<(8 * 8192 + 255) / 256, 256>>>(ss, 8 * 8192, 4, 1.f);
+    CK(hipMalloc(&refo, maxe * 4));
+    yh = (bf16*)malloc(maxe * 2);
+  }
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto& s : shapes) {
     if (only && !strstr(s.name, only)) continue;
@@ -54,8 +115,23 @@ int main(int argc, char** argv) {
     double us = ms * 1e3 / iters;
     double fl = 2.0 * s.B * a.Ho * a.Wo * s.cout * s.kh * s.kh * s.cin;
     double by = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)s.B * a.Ho * a.Wo * s.cout * (1 + s.res));
-    printf("%-26s variant %d  %8.1f us  %7.1f TF/s  %6.0f GB/s(min bytes)\n", s.name,
+    printf("%-26s variant %d  %8.1f us  %7.1f TF/s  %6.0f GB/s(min bytes)", s.name,
            conv_variant(a, s.kh, 2), us, fl / us / 1e6, by / us / 1e3);
+    if (check) {
+      const size_t n = (size_t)s.B * a.Ho * a.Wo * s.cout;
+      ref_conv<<<(n + 255) / 256, 256>>>(a, s.kh, s.s, s.p, refo);
+      CK(hipDeviceSynchronize());
+      std::vector<float> r(n);
+      CK(hipMemcpy(r.data(), refo, n * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(yh, y, n * 2, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (size_t i = 0; i < n; ++i) {
+        md = fmax(md, fabs((double)(float)yh[i] - r[i]));
+        mx = fmax(mx, fabs((double)r[i]));
+      }
+      printf("  check rel %.2e %s", md / mx, md / mx < 1e-2 ? "OK" : "FAIL");
+    }
+    printf("\n");
   }
   return 0;
 }
