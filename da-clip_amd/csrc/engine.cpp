@@ -468,6 +468,25 @@ struct UNetNet {
 
   const void* linattn(Run& r, const LA& la, const void* x, int C, int B, int H, int W) {
     const size_t M = (size_t)B * H * W;
+    if (C == 64 || C == 128) {
+      // Fused front half (linattn.hip): LN + to_qkv + context in one pass over x; q is
+      // written already softmaxed and scaled, so to_out is a plain per-image-weight GEMM.
+      T* q = r.alloc<T>(M * 128);
+      T* weff = r.alloc<T>((size_t)B * C * 128);
+      float* ws = r.alloc<float>(linear_attention_fused_ws_floats(B, H * W));
+      r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32;
+      if (!r.dry)
+        linear_attention_fused<T>(x, la.gpre, la.qkv.w, q, la.wout, weff, B, H * W, C, ws, r.st);
+      ConvW wo;
+      wo.w = weff; wo.b = la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
+      T* t = r.alloc<T>(M * C);
+      Epi eo;
+      eo.w_bstride = (long long)C * 128;
+      conv_call<T>(r, wo, q, 128, 128, nullptr, 0, B, H, W, 0, 1, 0, t, C, eo);
+      T* y = r.alloc<T>(M * C);
+      ln<T>(r, t, C, y, C, x, C, la.gout, nullptr, (int)M, C, 1e-5f);
+      return y;
+    }
     T* xn = r.alloc<T>(M * C);
     ln<T>(r, x, C, xn, C, nullptr, 0, la.gpre, nullptr, (int)M, C, 1e-5f);
     T* qkv = r.alloc<T>(M * 384);

@@ -71,6 +71,13 @@ void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t
 template <typename T>
 void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
                            float* ws, hipStream_t st);
+// Fused PreNorm + to_qkv + context (C in {64, 128}): writes q = softmax_d(q) * 32^-0.5 to
+// qout [B*HW][128] and W_eff to weff; ws: linear_attention_fused_ws_floats(B, HW) floats.
+template <typename T>
+void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, void* qout,
+                            const float* wout, void* weff, int B, int HW, int C, float* ws,
+                            hipStream_t st);
+size_t linear_attention_fused_ws_floats(int B, int HW);
 size_t linear_attention_ws_floats(int B, int HW);
 
 // Small fp32 dense layer for per-image vectors (time / prompt MLPs, ViT head):
