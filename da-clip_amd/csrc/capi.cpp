@@ -1,5 +1,9 @@
 // capi.cpp — extern "C" boundary of libdaclip_hip.so (declared in include/daclip_hip.h).
 // Every entry point converts exceptions into a negative DAC_E* code + dac_last_error().
+#include <cstdio>
+#include <algorithm>
+#include <array>
+#include <map>
 #include <cmath>
 #include <set>
 
@@ -253,11 +257,29 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
     auto& p = h->eng->prof;
     if (p.kernel_id < 0 || p.launches == 0) throw dac::Error(DAC_E_STATE, "nothing profiled");
     double tot = 0;
+    std::map<std::string, std::array<double, 3>> by;   // label -> count, ms, flops
     for (size_t i = 0; i < p.launches; ++i) {
       HIP_OK(hipEventSynchronize(p.ev[2 * i + 1]));
       float ms = 0;
       HIP_OK(hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]));
       tot += ms;
+      if (i < p.labels.size()) {
+        auto& v = by[p.labels[i]];
+        v[0] += 1; v[1] += ms; v[2] += p.lflops[i];
+      }
+    }
+    if (!by.empty()) {                                  // per-shape report (kernel_id ALL)
+      std::vector<std::pair<double, std::string>> rows;
+      for (auto& kv : by) {
+        char line[320];
+        snprintf(line, sizeof line, "%6.0f x %8.1f us = %8.2f ms  %7.1f TF/s  %s", kv.second[0],
+                 1e3 * kv.second[1] / kv.second[0], kv.second[1],
+                 kv.second[2] / (kv.second[1] * 1e-3) / 1e12, kv.first.c_str());
+        rows.push_back({kv.second[1], line});
+      }
+      std::sort(rows.rbegin(), rows.rend());
+      fprintf(stderr, "[dac conv profile] %zu launches, %.2f ms total\n", p.launches, tot);
+      for (auto& r : rows) fprintf(stderr, "  %s\n", r.second.c_str());
     }
     n = (int)p.launches;
     if (mean_ms) *mean_ms = tot / n;

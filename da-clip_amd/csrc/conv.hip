@@ -26,7 +26,10 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   const int Mg = batched ? a.Ho * a.Wo : a.B * a.Ho * a.Wo;
   const int gz = batched ? a.B : 1;
   const bool v2ok = V2 && a.zero && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
-  if (kh == 3 && v2ok && !batched && conv3_rw_host(a, 256) > 0) {
+  const int VEh = 16 / elem_bytes;
+  const bool epi_min = (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cout % VEh == 0 && a.ldy % VEh == 0 &&
+                       (!a.res1 || a.ldr1 % VEh == 0) && (!a.res2 || a.ldr2 % VEh == 0);
+  if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0) {
     if (a.Cout <= 64) return conv3_rw_host(a, 128) > 0 ? 6 : 10;
     if (conv3_rw_host(a, 128) > 0)
       return (long)(a.B * a.Ho * a.Wo / 128) * ((a.Cout + 127) / 128) >= 512 ? 7 : 11;

@@ -42,9 +42,39 @@ constexpr int epi_rows(int budget) {
   return best;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPR, class RowMap>
+// Epilogue feature set compiled into a kernel (EPK bits). A kernel that can only meet the
+// fast case (tile inside one image, SiLU / none, 16-byte aligned rows) compiles EPI_MIN and
+// stays small: the epilogue runs once per block, and every path compiled into it costs
+// instruction-cache fetches on that one pass.
+enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15 };
+
+// Per-channel epilogue terms of this lane's accumulator columns (bias, 1 + scale, shift) for a
+// tile inside image bimg; kernels that know bimg up front load them before the main loop.
+template <int TN> struct EpiTerms { float bi[TN], sc[TN], sh[TN]; };
+
+template <int TN>
+DEV EpiTerms<TN> epi_terms(const ConvArgs& a, int n0, int bimg, int colbase) {
+  EpiTerms<TN> e;
+  const int lr = threadIdx.x & 15;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + colbase + j * 16 + lr;
+    const bool ok = n < a.Cout;
+    e.bi[j] = (a.bias && ok) ? a.bias[n] : 0.f;
+    e.sc[j] = 1.f; e.sh[j] = 0.f;
+    if (a.ss && ok) {
+      const float* s = a.ss + (size_t)bimg * a.ss_ld;
+      e.sc[j] = s[n] + 1.f;
+      e.sh[j] = s[a.Cout + n];
+    }
+  }
+  return e;
+}
+
+template <typename T, int BM, int BN, int WGM, int WGN, int EPR, int EPK = EPI_ALL, class RowMap>
 DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
-                           char* smem, int M, const RowMap& rowmap, int n0, int HWo, int bimg) {
+                           char* smem, int M, const RowMap& rowmap, int n0, int HWo, int bimg,
+                           const EpiTerms<BN / WGN / 16>* pre = nullptr) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
   static_assert(EPR % WTM == 0 && BM % EPR == 0, "epilogue pass height");
   constexpr int NT = 64 * WGM * WGN;
@@ -53,31 +83,69 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
-  const bool geglu = a.act == ACT_GEGLU;
-  const bool fast = !geglu && bimg >= 0;
+  const bool geglu = (EPK & EPI_GEGLU) && a.act == ACT_GEGLU;
+  const bool fast = !(EPK & EPI_GENERAL) || (!geglu && bimg >= 0);
   float* tile = reinterpret_cast<float*>(smem);
-
-  // Fast path: all rows of the tile belong to image bimg -> per-channel terms in registers.
-  float sc[TN], sh[TN], bi[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    sc[j] = 1.f; sh[j] = 0.f; bi[j] = 0.f;
-    if (fast) {
-      const int n = n0 + wn * WTN + j * 16 + lr;
-      const bool ok = n < a.Cout;
-      bi[j] = (a.bias && ok) ? a.bias[n] : 0.f;
-      if (a.ss && ok) {
-        const float* s = a.ss + (size_t)bimg * a.ss_ld;
-        sc[j] = s[n] + 1.f;
-        sh[j] = s[a.Cout + n];
-      }
-    }
-  }
 
   T* y = reinterpret_cast<T*>(a.y);
   const T* r1 = reinterpret_cast<const T*>(a.res1);
   const T* r2 = reinterpret_cast<const T*>(a.res2);
+  // EPI_MIN kernels (single pass, vector rows): issue this thread's residual loads first, so
+  // their latency overlaps the accumulator math and LDS staging below.
+  constexpr bool PREF = EPK == EPI_MIN && EPR == BM;
+  constexpr int CPRF = BN / VE;
+  constexpr int NKP = PREF ? (BM * CPRF + NT - 1) / NT : 1;
+  u32x4 rv1[NKP], rv2[NKP];
+  if constexpr (PREF) {
+#pragma unroll
+    for (int k = 0; k < NKP; ++k) {
+      const int c = tid + k * NT;
+      const int m = rowmap(c / CPRF), n = n0 + (c % CPRF) * VE;
+      const bool ok = c < BM * CPRF && m < M && n < a.Cout;
+      rv1[k] = (r1 && ok) ? *reinterpret_cast<const u32x4*>(r1 + (size_t)m * a.ldr1 + n) : u32x4{0u, 0u, 0u, 0u};
+      rv2[k] = (r2 && ok) ? *reinterpret_cast<const u32x4*>(r2 + (size_t)m * a.ldr2 + n) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+
+  // Fast path: all rows of the tile belong to image bimg -> per-channel terms in registers.
+  EpiTerms<TN> et;
+  if (pre) et = *pre;
+  else if (fast) et = epi_terms<TN>(a, n0, bimg, wn * WTN);
+  else {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { et.bi[j] = 0.f; et.sc[j] = 1.f; et.sh[j] = 0.f; }
+  }
+  const float* bi = et.bi;
+  const float* sc = et.sc;
+  const float* sh = et.sh;
   const bool vec_ok = (a.ldy % VE == 0) && (!r1 || a.ldr1 % VE == 0) && (!r2 || a.ldr2 % VE == 0);
+  // Prefetched variant (PREF): chunk k of this thread.
+  auto emit_pre = [&](int k, int t, const float* src, int n) __attribute__((always_inline)) {
+    const int m = rowmap(t);
+    if (m >= M || n >= a.Cout) return;
+    float v[VE];
+#pragma unroll
+    for (int e = 0; e < VE; e += 4) {
+      const f32x4 q = *reinterpret_cast<const f32x4*>(src + e);
+      v[e] = q[0]; v[e + 1] = q[1]; v[e + 2] = q[2]; v[e + 3] = q[3];
+    }
+    const T* e1 = reinterpret_cast<const T*>(&rv1[k]);
+    const T* e2 = reinterpret_cast<const T*>(&rv2[k]);
+    if (r1) {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] += to_f(e1[e]);
+    }
+    if (r2) {
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] += to_f(e2[e]);
+    }
+    if (a.bbias) {
+      const float* bb = a.bbias + (size_t)bimg * a.bb_ld + n;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] += bb[e];
+    }
+    store_vec<T>(y + (size_t)m * a.ldy + n, v);
+  };
   // t: tile row, src: its LDS row.
   auto emit = [&](int t, const float* src, int n, int Cout) __attribute__((always_inline)) {
     const int m = rowmap(t);
@@ -89,7 +157,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
       v[e] = q[0]; v[e + 1] = q[1]; v[e + 2] = q[2]; v[e + 3] = q[3];
     }
     const int b = bimg >= 0 ? bimg : m / HWo;
-    if (vec_ok && n + VE <= Cout) {
+    if (!(EPK & EPI_SCALAR) || (vec_ok && n + VE <= Cout)) {
       float t1[VE];
       if (r1) {
         load_vec<T>(r1 + (size_t)m * a.ldr1 + n, t1);
@@ -107,7 +175,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
         for (int e = 0; e < VE; ++e) v[e] += bb[e];
       }
       store_vec<T>(y + (size_t)m * a.ldy + n, v);
-    } else {
+    } else if constexpr ((EPK & EPI_SCALAR) != 0) {
       for (int e = 0; e < VE && n + e < Cout; ++e) {
         float u = v[e];
         if (r1) u += to_f(r1[(size_t)m * a.ldr1 + n + e]);
@@ -130,10 +198,10 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
         for (int j = 0; j < TN; ++j) {
           float v = (acc[i][j][r] + bi[j]) * sc[j] + sh[j];
           if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if (a.act == ACT_GELU) v = gelu_f(v);
+          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_f(v);
           acc[i][j][r] = v;
         }
-  } else {
+  } else if constexpr ((EPK & EPI_GENERAL) != 0) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -163,7 +231,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
             if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
           }
           if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if (a.act == ACT_GELU) v = gelu_f(v);
+          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_f(v);
           acc[i][j][r] = v;
         }
       }
@@ -199,7 +267,8 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
       const int c = tid + k * NT;
       if (c >= nch) break;
       const int tl = c / CPR, cc = (c % CPR) * VE;
-      if (geglu) emit(r0 + tl, tile + tl * LDW + cc, n0 / 2 + cc, a.Cout / 2);
+      if constexpr (PREF) emit_pre(k, tl, tile + tl * LDW + cc, n0 + cc);
+      else if (geglu) emit(r0 + tl, tile + tl * LDW + cc, n0 / 2 + cc, a.Cout / 2);
       else emit(r0 + tl, tile + tl * LDW + cc, n0 + cc, a.Cout);
     }
   }

@@ -198,7 +198,8 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
-template <typename T, int BM, int BN, int WGM, int WGN, int STAGES, int KH, int KW, int S, int P>
+template <typename T, int BM, int BN, int WGM, int WGN, int STAGES, int KH, int KW, int S, int P,
+          int EPK = EPI_ALL>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 
@@ -480,6 +481,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const EpiTerms<TN> et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
 
   auto compute = [&](int buf) {
     const char* st = smem + buf * STAGE;
@@ -526,7 +528,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
-  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPI_MIN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
 }
 
 template <typename T, int KH, int KW, int S, int P>
@@ -542,7 +544,11 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     const int RW = conv3_rw(a);
-    if (v2ok && RW > 0 && a.w_bstride == 0) {
+    // v3's epilogue is compiled for the fast case only: SiLU / none, 16-byte rows.
+    const bool epi_min = (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cout % (16 / (int)sizeof(T)) == 0 &&
+                         a.ldy % (16 / (int)sizeof(T)) == 0 && (!a.res1 || a.ldr1 % (16 / (int)sizeof(T)) == 0) &&
+                         (!a.res2 || a.ldr2 % (16 / (int)sizeof(T)) == 0);
+    if (v2ok && RW > 0 && a.w_bstride == 0 && epi_min) {
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
       // blocks share a CU and one block's LDS-DMA latency hides behind another's MFMAs
       // (measured 10-24 % faster than one 8-wave block with 128-byte rows). Small grids
@@ -568,25 +574,33 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     }
   }
   if constexpr (V2) if (v2ok) {
+    // Minimal epilogue when every tile lies inside one image (tile rows divide H*W, or the
+    // per-image grid) and the tail is SiLU / none on 16-byte rows.
+    constexpr int VEh = 16 / sizeof(T);
+    const bool rows_ok = a.Cout % VEh == 0 && a.ldy % VEh == 0 && (!a.res1 || a.ldr1 % VEh == 0) &&
+                         (!a.res2 || a.ldr2 % VEh == 0);
+    const bool act_ok = a.act == ACT_NONE || a.act == ACT_SILU;
+    const int HWo = a.Ho * a.Wo;
+    auto minimal = [&](int BMv) { return rows_ok && act_ok && (batched || HWo % BMv == 0); };
+#define DAC_V2(BM_, BN_, WGM_, WGN_, ST_, THR_)                                                   \
+    {                                                                                            \
+      dim3 g((Mg + BM_ - 1) / BM_, (a.Cout + BN_ - 1) / BN_, gz);                                \
+      if (minimal(BM_))                                                                          \
+        conv2_kernel<T, BM_, BN_, WGM_, WGN_, ST_, KH, KW, S, P, EPI_MIN><<<g, THR_, 0, st>>>(a); \
+      else                                                                                       \
+        conv2_kernel<T, BM_, BN_, WGM_, WGN_, ST_, KH, KW, S, P, EPI_ALL><<<g, THR_, 0, st>>>(a); \
+      return;                                                                                    \
+    }
     if constexpr (KH == 1) if (a.K <= BKE) {
       // One K tile (1x1 over 64 bf16 channels): no pipeline to fill, so a single small
       // stage (128x64, 4 waves) keeps several blocks resident per CU and their load
       // latencies overlap (measured best of 256x128 x {1,2,3} stages, 128x128, 128x64).
-      dim3 g((Mg + 127) / 128, (a.Cout + 63) / 64, gz);
-      conv2_kernel<T, 128, 64, 2, 2, 1, KH, KW, S, P><<<g, 256, 0, st>>>(a);
-      return;
+      DAC_V2(128, 64, 2, 2, 1, 256)
     }
-    if (a.Cout <= 64) {
-      dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, gz);
-      conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P><<<g, 512, 0, st>>>(a);
-    } else if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) {
-      dim3 g((Mg + 255) / 256, (a.Cout + 127) / 128, gz);
-      conv2_kernel<T, 256, 128, 4, 2, 3, KH, KW, S, P><<<g, 512, 0, st>>>(a);
-    } else {
-      dim3 g((Mg + 127) / 128, (a.Cout + 127) / 128, gz);
-      conv2_kernel<T, 128, 128, 2, 2, 3, KH, KW, S, P><<<g, 256, 0, st>>>(a);
-    }
-    return;
+    if (a.Cout <= 64) DAC_V2(256, 64, 4, 2, 3, 512)
+    if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) DAC_V2(256, 128, 4, 2, 3, 512)
+    DAC_V2(128, 128, 2, 2, 3, 256)
+#undef DAC_V2
   }
   if (a.Cout <= 16 && a.act != ACT_GEGLU) {
     dim3 g((Mg + 255) / 256, (a.Cout + 15) / 16, gz);

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 
 namespace dac {
@@ -159,7 +160,8 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   r.flops += fl;
   Profiler* p = r.prof;
-  const bool timed = p && p->kernel_id == cw.kh * 100 + conv_variant(a, cw.kh, (int)sizeof(T));
+  const int cls = cw.kh * 100 + conv_variant(a, cw.kh, (int)sizeof(T));
+  const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == cls);
   if (r.dry) {
     if (timed) p->used++;
     return;
@@ -177,6 +179,14 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     p->used++;
     p->launches++;
     p->flops += fl;
+    if (p->kernel_id == Profiler::ALL) {
+      char lab[160];
+      snprintf(lab, sizeof lab, "c%d %3dx%-3d%s s%d %4d->%-4d%s%s%s%s", cls, Hs, Ws, up ? "^" : " ",
+               stride, cw.cin_real, cw.cout, e.res1 ? " +r" : "", e.res2 ? " +r2" : "",
+               e.ss ? " ss" : "", e.w_bstride ? " perimg" : "");
+      p->labels.push_back(lab);
+      p->lflops.push_back(fl);
+    }
     // Algorithmic HBM bytes: every operand touched once (input, weights, output, residuals).
     const double es = sizeof(T);
     p->bytes += es * ((double)B * Hs * Ws * cw.cin_real + (double)cw.cout * cw.kh * cw.kw * cw.cin +

@@ -83,7 +83,11 @@ struct Profiler {
   size_t used = 0;               // pairs recorded in the current pass
   double flops = 0, bytes = 0;   // algorithmic work of the recorded launches
   size_t launches = 0;
-  void begin_pass() { used = 0; flops = 0; bytes = 0; launches = 0; }
+  // kernel_id == ALL: every conv launch is timed and labelled by shape (per-shape report).
+  static constexpr int ALL = 999;
+  std::vector<std::string> labels;
+  std::vector<double> lflops;
+  void begin_pass() { used = 0; flops = 0; bytes = 0; launches = 0; labels.clear(); lflops.clear(); }
   ~Profiler();
 };
 
