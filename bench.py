@@ -57,6 +57,7 @@ def parse():
                    help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo, Cout<=64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
+    p.add_argument("--no-psnr", action="store_true", help="skip the bf16-vs-fp32 PSNR sample")
     p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")
     return p.parse_args()
 
@@ -101,6 +102,35 @@ def cpu_baseline(args, sd_unet, sd_clip):
                       f"per-image time = encode + {args.T} x step"}
 
 
+def psnr_sample(args, wu_keys, clip, unet_bf16, lq, img, dev):
+    """PSNR of the bf16 restore vs the fp32 (parity-mode) restore of image 0 at the bench
+    resolution, same contexts, same injected noise. The fp32 path reproduces the reference's
+    uint8 output bit-exactly on the T=100 golden fixture (tests/test_hip_parity.py)."""
+    from daclip_amd import synth
+    from daclip_amd.unet import ConditionalUNet
+    from daclip_amd.sde import IRSDE
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    t0 = time.perf_counter()
+    u32 = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype="fp32")
+    u32.load_state_dict(synth.synth_state_dict(wu_keys, 0))
+    ic, dc = clip.encode_image(img, control=True)
+    R = lq.shape[-1]
+    ns = torch.from_numpy(synth.synth_noise((1, 3, R, R), seed=7, tag="psnr_ns")).to(dev)
+    zs = torch.from_numpy(synth.synth_noise((args.T, 1, 3, R, R), seed=8, tag="psnr_z")).to(dev)
+    outs = {}
+    for name, m in (("bf16", unet_bf16), ("fp32", u32)):
+        s = IRSDE(max_sigma=50, T=args.T, schedule="cosine", eps=0.005)
+        s.set_model(m)
+        s.set_mu(lq)
+        x = s.noise_state(lq, noise=ns)
+        outs[name] = tensor2img(s.reverse_posterior(x, noises=zs, text_context=dc, image_context=ic)[0])
+    gt = tensor2img(lq[0])
+    return {"bf16_vs_fp32_db": round(float(calculate_psnr(outs["bf16"], outs["fp32"])), 3),
+            "delta_db_on_lq": round(float(calculate_psnr(outs["bf16"], gt) - calculate_psnr(outs["fp32"], gt)), 5),
+            "sample": f"image 0, {R}x{R}, T={args.T}, same contexts + injected noise; fp32 = parity path "
+                      f"({time.perf_counter() - t0:.1f}s)"}
+
+
 def main():
     args = parse()
     ws, rank, local = setup_dist(args)
@@ -120,7 +150,7 @@ def main():
 
     unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype=args.dtype)
     unet.load_state_dict(wu)
-    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, device=dev, dtype=args.dtype)
+    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, device=dev, dtype=args.dtype, with_text=False)
     clip.load_state_dict(wc, strict=False)
     del wu, wc
     sde = IRSDE(max_sigma=50, T=args.T, schedule="cosine", eps=0.005)
@@ -187,6 +217,10 @@ def main():
                                                        _lib.ctypes.byref(by)), "profile_read")
         h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
 
+    psnr = None
+    if rank == 0 and not args.no_psnr and args.dtype == "bf16":
+        psnr = psnr_sample(args, wu_keys=uspec, clip=clip, unet_bf16=unet, lq=lq[:1], img=img4clip[:1], dev=dev)
+
     if rank == 0:
         images = n_glob * args.steps
         ach = fl.value / (mean_ms.value * 1e-3) / 1e12 if n_launch > 0 else None
@@ -220,7 +254,7 @@ def main():
                           "sampler": "posterior", "parallelism": f"dp{ws}"},
                "model_tflop_per_image": round(total_tf, 3),
                "whole_path_tflops": round(total_tf * images / el, 1),
-               "roofline": roof, "outputs_finite": finite}
+               "roofline": roof, "outputs_finite": finite, "psnr": psnr}
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, synth.synth_state_dict(uspec, 0),
                                                synth.synth_state_dict(cspec, 0))

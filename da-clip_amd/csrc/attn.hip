@@ -157,54 +157,67 @@ void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, 
 }
 
 // ------------------------------------------------------------------------------ small MHA
-template <typename T>
-__global__ void __launch_bounds__(64) small_mha_kernel(const T* __restrict__ qkv, T* o, int L,
-                                                       int H, int D) {
-  extern __shared__ float sm[];               // K [L][D+1], V [L][D]
+// Short-sequence MHA (ViT tokens L = 50 / 257, CLIP text L = 77), head dim 64 (or 32): one thread per
+// query, K / V of the (image, head) staged in LDS as fp32, single-pass online softmax (running
+// max + rescaled accumulator, so any L fits in registers); `causal` masks keys t > query
+// (the text tower's additive -inf upper triangle, transformer.py:751-757).
+template <typename T, int D>
+__global__ void __launch_bounds__(64) small_mha_kernel(const T* __restrict__ qkv, T* o, int L, int H,
+                                                       int causal) {
+  extern __shared__ float sm[];               // K [L][D], V [L][D]
   const int b = blockIdx.y, h = blockIdx.x;
   const int ld = 3 * H * D;
   const T* base = qkv + (size_t)b * L * ld;
   float* sk = sm;
-  float* sv = sm + L * (D + 1);
-  for (int i = threadIdx.x; i < L * D; i += 64) {
-    const int t = i / D, d = i - t * D;
-    sk[t * (D + 1) + d] = to_f(base[(size_t)t * ld + H * D + h * D + d]);
-    sv[t * D + d] = to_f(base[(size_t)t * ld + 2 * H * D + h * D + d]);
+  float* sv = sm + L * D;
+  for (int i = threadIdx.x; i < L * (D / 4); i += 64) {
+    const int t = i / (D / 4), d = (i - t * (D / 4)) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sk[t * D + d + e] = to_f(base[(size_t)t * ld + H * D + h * D + d + e]);
+      sv[t * D + d + e] = to_f(base[(size_t)t * ld + 2 * H * D + h * D + d + e]);
+    }
   }
   __syncthreads();
   const float scale = rsqrtf((float)D);
-  for (int qi = threadIdx.x; qi < L; qi += 64) {
-    float qv[64];
-    for (int d = 0; d < D; ++d) qv[d] = to_f(base[(size_t)qi * ld + h * D + d]) * scale;
-    float sc[64];
-    float mx = -INFINITY;
-    for (int t = 0; t < L; ++t) {
+  for (int qi = blockIdx.z * 64 + threadIdx.x; qi < L; qi += 64 * gridDim.z) {
+    float qv[D], acc[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) { qv[d] = to_f(base[(size_t)qi * ld + h * D + d]) * scale; acc[d] = 0.f; }
+    float mx = -INFINITY, sum = 0.f;
+    const int tend = causal ? qi + 1 : L;
+    for (int t = 0; t < tend; ++t) {
+      const float* kr = sk + t * D;
       float a = 0.f;
-      for (int d = 0; d < D; ++d) a += qv[d] * sk[t * (D + 1) + d];
-      sc[t] = a;
-      mx = fmaxf(mx, a);
+#pragma unroll
+      for (int d = 0; d < D; ++d) a += qv[d] * kr[d];
+      const float mn = fmaxf(mx, a);
+      const float c = expf(mx - mn), p = expf(a - mn);
+      sum = sum * c + p;
+      const float* vr = sv + t * D;
+#pragma unroll
+      for (int d = 0; d < D; ++d) acc[d] = acc[d] * c + p * vr[d];
+      mx = mn;
     }
-    float sum = 0.f;
-    for (int t = 0; t < L; ++t) { sc[t] = expf(sc[t] - mx); sum += sc[t]; }
     const float inv = 1.f / sum;
     T* out = o + ((size_t)b * L + qi) * (H * D) + h * D;
-    for (int d = 0; d < D; ++d) {
-      float a = 0.f;
-      for (int t = 0; t < L; ++t) a += sc[t] * sv[t * D + d];
-      out[d] = from_f<T>(a * inv);
-    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) out[d] = from_f<T>(acc[d] * inv);
   }
 }
 
 template <typename T>
-void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t st) {
-  const size_t smem = (size_t)L * (2 * D + 1) * sizeof(float);
-  small_mha_kernel<T><<<dim3(H, B), 64, smem, st>>>((const T*)qkv, (T*)o, L, H, D);
+void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal, hipStream_t st) {
+  const size_t smem = (size_t)L * 2 * D * sizeof(float);
+  const dim3 g(H, B, (L + 63) / 64);
+  if (D == 64) small_mha_kernel<T, 64><<<g, 64, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
+  else if (D == 32) small_mha_kernel<T, 32><<<g, 64, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
+  else __builtin_trap();
 }
 
 #define INST(T)                                                                           \
   template void flash_attn_d32<T>(const void*, void*, int, int, int, float, hipStream_t); \
-  template void small_mha<T>(const void*, void*, int, int, int, int, hipStream_t);
+  template void small_mha<T>(const void*, void*, int, int, int, int, int, hipStream_t);
 INST(float)
 INST(bf16)
 #undef INST

@@ -43,6 +43,7 @@ int guard(dac_handle* h, F&& f) {
 // open_clip/model.py:203-213, daclip_model.py:24.
 bool ignorable(const dac_handle* h, const std::string& k) {
   if (!h->cfg.vit) return false;
+  if (h->cfg.text) return k == "clip.logit_scale" || k == "logit_scale";
   static const char* pre[] = {"clip.transformer.", "clip.token_embedding.", "clip.ln_final.",
                               "clip.positional_embedding", "clip.text_projection",
                               "clip.logit_scale", "logit_scale"};
@@ -156,6 +157,26 @@ int dac_encode_image(dac_handle* h, const float* img, int B, float* image_ctx, f
     need_ready(h);
     if (!img || !image_ctx || !degra_ctx || B < 1) throw dac::Error(DAC_E_ARG, "bad argument");
     h->eng->encode(img, B, image_ctx, degra_ctx, (hipStream_t)stream);
+    return DAC_OK;
+  });
+}
+
+int dac_encode_text(dac_handle* h, const int64_t* tokens, int N, float* text_features, void* stream) {
+  return guard(h, [&]() -> int {
+    need_ready(h);
+    if (!tokens || !text_features || N < 1) throw dac::Error(DAC_E_ARG, "bad argument");
+    h->eng->encode_text(tokens, N, text_features, (hipStream_t)stream);
+    return DAC_OK;
+  });
+}
+
+int dac_degradation_probs(dac_handle* h, const float* degra, const float* text_features, int B, int K,
+                          int E, float* probs, int32_t* argmax, void* stream) {
+  return guard(h, [&]() -> int {
+    if (!degra || !text_features || !probs || !argmax || B < 1 || K < 1 || K > 64 || E < 1)
+      throw dac::Error(DAC_E_ARG, "bad argument (1 <= K <= 64)");
+    dac::degradation_probs(degra, text_features, B, K, E, probs, argmax, (hipStream_t)stream);
+    HIP_OK(hipGetLastError());
     return DAC_OK;
   });
 }

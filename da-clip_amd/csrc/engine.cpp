@@ -632,12 +632,63 @@ struct VitNet {
   struct Block { const float *l1w, *l1b, *l2w, *l2b; ConvW qkv, out, fc, proj; };
   struct Tower { ConvW conv1; const float *cls, *pos, *prew, *preb, *postw, *postb, *projT;
                  std::vector<Block> blocks; std::vector<ConvW> zero; };
+  // CLIP text tower (model.py:203-211, 237-249): token / positional embeddings (fp32 tables),
+  // causal ResidualAttentionBlocks, ln_final, text_projection (transposed, fp32).
+  struct TextTower { const float *tok = nullptr, *pos = nullptr, *lnw = nullptr, *lnb = nullptr,
+                     *projT = nullptr; std::vector<Block> blocks; };
   dac_config cfg;
   int S, P, D, layers, heads, hd, mlp, E, G, L;
+  int Lt = 0, Vt = 0, Dt = 0, Ht = 0, layers_t = 0;
   Tower main, ctl;
+  TextTower txt;
   explicit VitNet(const dac_config& c) : cfg(c) {
     S = c.image_size; P = c.patch_size; D = c.width; layers = c.layers; hd = c.head_width;
     heads = D / hd; mlp = c.mlp_width; E = c.embed_dim; G = S / P; L = G * G + 1;
+    if (c.text) {
+      Lt = c.context_length; Vt = c.vocab_size; Dt = c.text_width; Ht = c.text_heads;
+      layers_t = c.text_layers;
+    }
+  }
+  Block load_block(Packer<T>& Pk, const std::string& q, int Dm, int mlpw) {
+    Block b;
+    b.l1w = Pk.f32(q + "ln_1.weight", {Dm});
+    b.l1b = Pk.f32(q + "ln_1.bias", {Dm});
+    b.qkv = Pk.linear(q + "attn.in_proj_weight", 3 * Dm, Dm, q + "attn.in_proj_bias");
+    b.out = Pk.linear(q + "attn.out_proj.weight", Dm, Dm, q + "attn.out_proj.bias");
+    b.l2w = Pk.f32(q + "ln_2.weight", {Dm});
+    b.l2b = Pk.f32(q + "ln_2.bias", {Dm});
+    b.fc = Pk.linear(q + "mlp.c_fc.weight", mlpw, Dm, q + "mlp.c_fc.bias");
+    b.proj = Pk.linear(q + "mlp.c_proj.weight", Dm, mlpw, q + "mlp.c_proj.bias");
+    return b;
+  }
+  // ResidualAttentionBlock.forward (transformer.py:232-244) on Mt = Bs * Ls token rows:
+  // x += attn(ln_1(x)); x += mlp(ln_2(x)) [+ res2, the controlled tower's control.pop()].
+  T* block(Run& r, const Block& b, const void* x, int Bs, int Ls, int Dm, int Hm, int mlpw, int causal,
+           const void* res2) {
+    const size_t Mt = (size_t)Bs * Ls;
+    T* a = r.alloc<T>(Mt * Dm);
+    ln<T>(r, x, Dm, a, Dm, nullptr, 0, b.l1w, b.l1b, (int)Mt, Dm, 1e-5f);
+    T* qkv = r.alloc<T>(Mt * 3 * Dm);
+    conv_call<T>(r, b.qkv, a, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, qkv, 3 * Dm, Epi());
+    T* o = r.alloc<T>(Mt * Dm);
+    r.flops += 4.0 * Bs * (double)Ls * Ls * Dm;
+    if (!r.dry) small_mha<T>(qkv, o, Bs, Ls, Hm, Dm / Hm, causal, r.st);
+    T* x2 = r.alloc<T>(Mt * Dm);
+    Epi e1;
+    e1.res1 = x; e1.ldr1 = Dm;
+    conv_call<T>(r, b.out, o, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x2, Dm, e1);
+    T* a2 = r.alloc<T>(Mt * Dm);
+    ln<T>(r, x2, Dm, a2, Dm, nullptr, 0, b.l2w, b.l2b, (int)Mt, Dm, 1e-5f);
+    T* f = r.alloc<T>(Mt * mlpw);
+    Epi eg;
+    eg.act = ACT_GELU;
+    conv_call<T>(r, b.fc, a2, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, f, mlpw, eg);
+    T* x3 = r.alloc<T>(Mt * Dm);
+    Epi e3;
+    e3.res1 = x2; e3.ldr1 = Dm;
+    if (res2) { e3.res2 = res2; e3.ldr2 = Dm; }
+    conv_call<T>(r, b.proj, f, mlpw, mlpw, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x3, Dm, e3);
+    return x3;
   }
   Tower load_tower(Packer<T>& Pk, const std::string& p, bool control) {
     Tower t;
@@ -651,17 +702,7 @@ struct VitNet {
     t.projT = Pk.f32_t(p + "proj", D, E);
     const std::string rb = p + (control ? "transformer.transformer.resblocks." : "transformer.resblocks.");
     for (int l = 0; l < layers; ++l) {
-      const std::string q = rb + std::to_string(l) + ".";
-      Block b;
-      b.l1w = Pk.f32(q + "ln_1.weight", {D});
-      b.l1b = Pk.f32(q + "ln_1.bias", {D});
-      b.qkv = Pk.linear(q + "attn.in_proj_weight", 3 * D, D, q + "attn.in_proj_bias");
-      b.out = Pk.linear(q + "attn.out_proj.weight", D, D, q + "attn.out_proj.bias");
-      b.l2w = Pk.f32(q + "ln_2.weight", {D});
-      b.l2b = Pk.f32(q + "ln_2.bias", {D});
-      b.fc = Pk.linear(q + "mlp.c_fc.weight", mlp, D, q + "mlp.c_fc.bias");
-      b.proj = Pk.linear(q + "mlp.c_proj.weight", D, mlp, q + "mlp.c_proj.bias");
-      t.blocks.push_back(b);
+      t.blocks.push_back(load_block(Pk, rb + std::to_string(l) + ".", D, mlp));
       if (control)
         t.zero.push_back(Pk.linear(p + "transformer.zero_modules." + std::to_string(l) + ".weight",
                                    D, D, p + "transformer.zero_modules." + std::to_string(l) + ".bias"));
@@ -680,6 +721,34 @@ struct VitNet {
     }
     main = load_tower(Pk, "clip.visual.", false);
     ctl = load_tower(Pk, "visual_control.", true);
+    if (cfg.text) {
+      txt.tok = Pk.f32("clip.token_embedding.weight", {Vt, Dt});
+      txt.pos = Pk.f32("clip.positional_embedding", {Lt, Dt});
+      for (int l = 0; l < layers_t; ++l)
+        txt.blocks.push_back(load_block(Pk, "clip.transformer.resblocks." + std::to_string(l) + ".", Dt, 4 * Dt));
+      txt.lnw = Pk.f32("clip.ln_final.weight", {Dt});
+      txt.lnb = Pk.f32("clip.ln_final.bias", {Dt});
+      txt.projT = Pk.f32_t("clip.text_projection", Dt, E);
+    }
+  }
+  // CLIP.encode_text (model.py:237-249): the EOT row is gathered before ln_final (a per-row
+  // op), then projected.
+  void encode_text(Run& r, const int64_t* tokens, int N, float* out) {
+    const size_t Mt = (size_t)N * Lt;
+    T* x = r.alloc<T>(Mt * Dt);
+    if (!r.dry) text_embed<T>(tokens, txt.tok, txt.pos, x, N, Lt, Dt, Vt, r.st);
+    const void* cur = x;
+    for (int l = 0; l < layers_t; ++l) cur = block(r, txt.blocks[l], cur, N, Lt, Dt, Ht, 4 * Dt, 1, nullptr);
+    T* pooled = r.alloc<T>((size_t)N * Dt);
+    if (!r.dry) eot_gather<T>(tokens, cur, pooled, N, Lt, Dt, r.st);
+    T* pn = r.alloc<T>((size_t)N * Dt);
+    ln<T>(r, pooled, Dt, pn, Dt, nullptr, 0, txt.lnw, txt.lnb, N, Dt, 1e-5f);
+    float* pf = r.alloc<float>((size_t)N * Dt);
+    r.flops += 2.0 * N * Dt * E;
+    if (!r.dry) {
+      rows_to_f32<T>(pn, Dt, pf, N, Dt, r.st);
+      small_linear(pf, Dt, txt.projT, nullptr, out, E, N, Dt, E, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
+    }
   }
   void tower(Run& r, const Tower& tw, const void* xin, int B, bool control,
              std::vector<const void*>* hid_out, const std::vector<const void*>* hid_in,
@@ -693,29 +762,8 @@ struct VitNet {
     T* x = r.alloc<T>(Mt * D);
     ln<T>(r, tok, D, x, D, nullptr, 0, tw.prew, tw.preb, (int)Mt, D, 1e-5f);
     for (int l = 0; l < layers; ++l) {
-      const Block& b = tw.blocks[l];
-      T* a = r.alloc<T>(Mt * D);
-      ln<T>(r, x, D, a, D, nullptr, 0, b.l1w, b.l1b, (int)Mt, D, 1e-5f);
-      T* qkv = r.alloc<T>(Mt * 3 * D);
-      conv_call<T>(r, b.qkv, a, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, qkv, 3 * D, Epi());
-      T* o = r.alloc<T>(Mt * D);
-      r.flops += 4.0 * B * (double)L * L * D;
-      if (!r.dry) small_mha<T>(qkv, o, B, L, heads, hd, r.st);
-      T* x2 = r.alloc<T>(Mt * D);
-      Epi e1;
-      e1.res1 = x; e1.ldr1 = D;
-      conv_call<T>(r, b.out, o, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x2, D, e1);
-      T* a2 = r.alloc<T>(Mt * D);
-      ln<T>(r, x2, D, a2, D, nullptr, 0, b.l2w, b.l2b, (int)Mt, D, 1e-5f);
-      T* f = r.alloc<T>(Mt * mlp);
-      Epi eg;
-      eg.act = ACT_GELU;
-      conv_call<T>(r, b.fc, a2, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, f, mlp, eg);
-      T* x3 = r.alloc<T>(Mt * D);
-      Epi e3;
-      e3.res1 = x2; e3.ldr1 = D;
-      if (hid_in) { e3.res2 = (*hid_in)[layers - 1 - l]; e3.ldr2 = D; }   // control.pop()
-      conv_call<T>(r, b.proj, f, mlp, mlp, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x3, D, e3);
+      T* x3 = block(r, tw.blocks[l], x, B, L, D, heads, mlp, 0,
+                    hid_in ? (*hid_in)[layers - 1 - l] : nullptr);        // control.pop()
       if (control) {
         T* hz = r.alloc<T>(Mt * D);
         conv_call<T>(r, tw.zero[l], x3, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, hz, D, Epi());
@@ -755,9 +803,13 @@ class EngineT : public Engine {
     HIP_OK(hipMemset(zero_page, 0, 256));
     if (c.unet) unet = std::make_unique<UNetNet<T>>(c);
     if (c.vit) {
-      if (c.image_size % c.patch_size || c.width % c.head_width || c.head_width > 64 ||
-          (c.image_size / c.patch_size) * (c.image_size / c.patch_size) + 1 > 64)
-        throw Error(DAC_E_ARG, "unsupported vision config (needs <= 64 tokens, head_width <= 64)");
+      if (c.image_size % c.patch_size || c.width % c.head_width || (c.head_width != 64 && c.head_width != 32) ||
+          (c.image_size / c.patch_size) * (c.image_size / c.patch_size) + 1 > 320)
+        throw Error(DAC_E_ARG, "unsupported vision config (needs <= 320 tokens, head_width 32 or 64)");
+      if (c.text && (c.text_heads < 1 || c.text_width % c.text_heads || c.context_length < 1 ||
+                     c.context_length > 320 || c.vocab_size < 1 || c.text_layers < 1 ||
+                     (c.text_width / c.text_heads != 64 && c.text_width / c.text_heads != 32)))
+        throw Error(DAC_E_ARG, "unsupported text config (head width 32 or 64, context <= 320)");
       vit = std::make_unique<VitNet<T>>(c);
     }
   }
@@ -873,6 +925,22 @@ class EngineT : public Engine {
     Run r = live(st);
     arena.reset();
     vit->encode(r, img, B, ic, dc);
+    HIP_OK(hipGetLastError());
+  }
+
+  // ------------------------------------------------------------------ text
+  void encode_text(const int64_t* tokens, int N, float* out, hipStream_t st) override {
+    need(vit != nullptr && cfg.text, "handle has no text tower");
+    HIP_OK(hipSetDevice(dev));
+    Arena a;
+    Run d;
+    d.dry = true;
+    d.ar = &a;
+    vit->encode_text(d, nullptr, N, nullptr);
+    ensure_arena(a.peak + (1 << 20));
+    Run r = live(st);
+    arena.reset();
+    vit->encode_text(r, tokens, N, out);
     HIP_OK(hipGetLastError());
   }
 

@@ -131,6 +131,7 @@ class Engine {
   virtual ~Engine() = default;
   virtual void finalize(WStore& w) = 0;
   virtual void encode(const float* img, int B, float* ic, float* dc, hipStream_t st) = 0;
+  virtual void encode_text(const int64_t* tokens, int N, float* out, hipStream_t st) = 0;
   virtual void unet_forward(const float* xt, const float* mu, float t, const float* tc,
                             const float* icx, int B, int H, int W, float* eps,
                             hipStream_t st) = 0;

@@ -57,9 +57,20 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
 template <typename T>
 void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st);
 
-// nn.MultiheadAttention core for the ViT (L <= 64 tokens, D = 64 or 32).
+// CLIP text tower helpers: token + positional embedding gather (ids outside [0, V) -> NaN),
+// EOT-row gather (position of the highest id per sequence), degradation-class scoring.
 template <typename T>
-void small_mha(const void* qkv, void* o, int B, int L, int H, int D, hipStream_t st);
+void text_embed(const int64_t* tok, const float* emb, const float* pos, void* x, int N, int L, int D, int V,
+                hipStream_t st);
+template <typename T>
+void eot_gather(const int64_t* tok, const void* x, void* out, int N, int L, int D, hipStream_t st);
+void degradation_probs(const float* degra, const float* text, int B, int K, int E, float* probs,
+                       int32_t* argmax, hipStream_t st);
+
+// nn.MultiheadAttention core for short sequences (ViT / CLIP text), head dim D = 64, any L;
+// causal != 0 applies the text tower's causal mask.
+template <typename T>
+void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal, hipStream_t st);
 
 // LinearAttention (module_util.py:170-185) context on qkv [B*HW, 384] (q | k | v):
 //   la_kmax   : per (image, chunk) channel max of k

@@ -286,4 +286,106 @@ INST(float)
 INST(bf16)
 #undef INST
 
+// --------------------------------------------------------------------------- text tower
+template <typename T>
+__global__ void text_embed_kernel(const int64_t* tok, const float* emb, const float* pos, T* x, int N,
+                                  int L, int D, int V) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)N * L * D) return;
+  const int d = (int)(i % D);
+  const size_t nl = i / D;
+  const int l = (int)(nl % L);
+  const int64_t id = tok[nl];
+  const bool ok = id >= 0 && id < V;
+  const float v = ok ? emb[(size_t)id * D + d] + pos[(size_t)l * D + d] : __builtin_nanf("");
+  x[i] = from_f<T>(v);
+}
+
+template <typename T>
+void text_embed(const int64_t* tok, const float* emb, const float* pos, void* x, int N, int L, int D, int V,
+                hipStream_t st) {
+  const size_t n = (size_t)N * L * D;
+  text_embed_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(tok, emb, pos, (T*)x, N, L, D, V);
+}
+
+// One block per sequence: first position of the largest id (torch.argmax), copy that row.
+template <typename T>
+__global__ void __launch_bounds__(64) eot_gather_kernel(const int64_t* tok, const T* x, T* out, int L, int D) {
+  const int n = blockIdx.x, lane = threadIdx.x;
+  int64_t best = INT64_MIN;
+  int bi = L;
+  for (int l = lane; l < L; l += 64) {
+    const int64_t v = tok[(size_t)n * L + l];
+    if (v > best) { best = v; bi = l; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  for (int d = lane; d < D; d += 64) out[(size_t)n * D + d] = x[((size_t)n * L + bi) * D + d];
+}
+
+template <typename T>
+void eot_gather(const int64_t* tok, const void* x, void* out, int N, int L, int D, hipStream_t st) {
+  eot_gather_kernel<T><<<N, 64, 0, st>>>(tok, (const T*)x, (T*)out, L, D);
+}
+
+// One block (256 threads) per image: cosine scores vs K class texts, x100, softmax, argmax.
+__global__ void __launch_bounds__(256) degra_probs_kernel(const float* degra, const float* text, int K,
+                                                          int E, float* probs, int32_t* amax) {
+  __shared__ float red[8];
+  __shared__ float sc[64];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* d = degra + (size_t)b * E;
+  auto block_sum = [&](float v) {
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  float dd = 0.f;
+  for (int e = tid; e < E; e += 256) dd += d[e] * d[e];
+  const float dn = sqrtf(block_sum(dd));
+  for (int k = 0; k < K; ++k) {
+    const float* t = text + (size_t)k * E;
+    float tt = 0.f, dt = 0.f;
+    for (int e = tid; e < E; e += 256) { tt += t[e] * t[e]; dt += d[e] * t[e]; }
+    const float tn = sqrtf(block_sum(tt));
+    const float dot = block_sum(dt);
+    if (tid == 0) sc[k] = 100.f * (dot / (dn * tn));
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float m = -INFINITY;
+    int mi = 0;
+    for (int k = 0; k < K; ++k)
+      if (sc[k] > m) { m = sc[k]; mi = k; }
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += expf(sc[k] - m);
+    // argmax over the probabilities themselves (torch.argmax(probs), first maximum).
+    float pm = -1.f;
+    for (int k = 0; k < K; ++k) {
+      const float pk = expf(sc[k] - m) / s;
+      probs[(size_t)b * K + k] = pk;
+      if (pk > pm) { pm = pk; mi = k; }
+    }
+    amax[b] = mi;
+  }
+}
+
+void degradation_probs(const float* degra, const float* text, int B, int K, int E, float* probs,
+                       int32_t* argmax, hipStream_t st) {
+  degra_probs_kernel<<<B, 256, 0, st>>>(degra, text, K, E, probs, argmax);
+}
+
+#define TINST(T)                                                                                 \
+  template void text_embed<T>(const int64_t*, const float*, const float*, void*, int, int, int, int, \
+                              hipStream_t);                                                      \
+  template void eot_gather<T>(const int64_t*, const void*, void*, int, int, int, hipStream_t);
+TINST(float)
+TINST(bf16)
+#undef TINST
+
 }  // namespace dac

@@ -24,7 +24,8 @@ DAC_COSINE, DAC_LINEAR, DAC_CONSTANT = 0, 1, 2
 DAC_E_MISSING, DAC_E_KEY = -3, -2
 
 EXPORTS = ["dac_create", "dac_destroy", "dac_set_weight", "dac_finalize_weights",
-           "dac_encode_image", "dac_unet_forward", "dac_sde_schedule", "dac_sde_reverse",
+           "dac_encode_image", "dac_encode_text", "dac_degradation_probs", "dac_unet_forward",
+           "dac_sde_schedule", "dac_sde_reverse",
            "dac_set_noise_offset", "dac_posterior_step", "dac_unet_flops", "dac_encode_flops", "dac_profile_enable",
            "dac_profile_read", "dac_last_error"]
 
@@ -36,7 +37,9 @@ class DacConfig(ctypes.Structure):
                 ("use_image_context", ctypes.c_int), ("vit", ctypes.c_int),
                 ("image_size", ctypes.c_int), ("patch_size", ctypes.c_int),
                 ("width", ctypes.c_int), ("layers", ctypes.c_int), ("head_width", ctypes.c_int),
-                ("mlp_width", ctypes.c_int), ("embed_dim", ctypes.c_int)]
+                ("mlp_width", ctypes.c_int), ("embed_dim", ctypes.c_int),
+                ("text", ctypes.c_int), ("context_length", ctypes.c_int), ("vocab_size", ctypes.c_int),
+                ("text_width", ctypes.c_int), ("text_heads", ctypes.c_int), ("text_layers", ctypes.c_int)]
 
 
 _lib = None
@@ -57,6 +60,8 @@ def lib() -> ctypes.CDLL:
         "dac_set_weight": (I, [P, ctypes.c_char_p, P, ctypes.POINTER(ctypes.c_int64), I, I]),
         "dac_finalize_weights": (I, [P]),
         "dac_encode_image": (I, [P, P, I, P, P, P]),
+        "dac_encode_text": (I, [P, P, I, P, P]),
+        "dac_degradation_probs": (I, [P, P, P, I, I, I, P, P, P]),
         "dac_unet_forward": (I, [P, P, P, F, P, P, I, I, I, P, P]),
         "dac_sde_schedule": (I, [P, F, I, I, F, P, F]),
         "dac_sde_reverse": (I, [P, I, P, P, P, P, I, I, I, I, P, U64, P]),

@@ -2,7 +2,9 @@
 
 Mirrors open_clip/factory.py:88-106 (load_state_dict / load_checkpoint key handling),
 :109-269 (create_model, daclip branch 190-192, local-path checkpoint 231-241),
-:365-404 (create_model_from_pretrained) and daclip_model.py:46-55 (encode_image).
+:365-404 (create_model_from_pretrained), daclip_model.py:46-55 (encode_image) and :125-126
+(encode_text -> model.py:237-249), plus the degradation-class scoring of
+da-clip/src/evaluate_daclip.py:45-50, 78-84.
 """
 from __future__ import annotations
 
@@ -26,23 +28,34 @@ def load_state_dict(checkpoint_path: str, map_location="cpu"):
     return sd
 
 
-def vision_config(v: arch.VisionConfig) -> _lib.DacConfig:
+def vision_config(v: arch.VisionConfig, t: Optional[arch.TextConfig] = None) -> _lib.DacConfig:
     c = _lib.DacConfig()
     c.vit = 1
     c.image_size, c.patch_size, c.width = v.image_size, v.patch_size, v.width
     c.layers, c.head_width = v.layers, v.head_width
     c.mlp_width = int(v.width * v.mlp_ratio)
     c.embed_dim = v.embed_dim
+    if t is not None:
+        c.text = 1
+        c.context_length, c.vocab_size = t.context_length, t.vocab_size
+        c.text_width, c.text_heads, c.text_layers = t.width, t.heads, t.layers
     return c
+
+
+def _is_text_key(k: str) -> bool:
+    return k.startswith(("clip.transformer.", "clip.token_embedding.", "clip.ln_final.",
+                         "clip.positional_embedding", "clip.text_projection"))
 
 
 class DaCLIP:
     """DaCLIP(CLIP) image side: frozen clip.visual + controller visual_control."""
 
     def __init__(self, vision: arch.VisionConfig = arch.VIT_B_32,
-                 text: arch.TextConfig = arch.TEXT_B_32, device="cuda", dtype="fp32"):
+                 text: arch.TextConfig = arch.TEXT_B_32, device="cuda", dtype="fp32",
+                 with_text: bool = True):
         self.vision, self.text = vision, text
-        self._h = _lib.Handle(torch.device(device), dtype, vision_config(vision))
+        self.with_text = with_text
+        self._h = _lib.Handle(torch.device(device), dtype, vision_config(vision, text if with_text else None))
         self.device = self._h.device
         self.dtype = dtype
         self.visual = self          # exposes .image_size like VisionTransformer
@@ -75,8 +88,9 @@ class DaCLIP:
                 continue
             if k.startswith("visual.") and ("clip." + k) in state_dict:
                 continue      # alias of clip.visual.* (same tensor)
-            if not (k.startswith("clip.visual.") or k.startswith("visual")):
-                continue      # text tower / logit scales: not on the image path
+            if not (k.startswith("clip.visual.") or k.startswith("visual") or
+                    (self.with_text and _is_text_key(k))):
+                continue      # logit scales (and the text tower when built without it)
             v = state_dict[k]
             t = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
             if tuple(t.shape) != tuple(spec[k]):
@@ -87,7 +101,8 @@ class DaCLIP:
         return missing, unexpected
 
     def load_synthetic(self, seed: int = 0):
-        spec = {k: s for k, s in self.state_spec().items() if "visual" in k}
+        spec = {k: s for k, s in self.state_spec().items()
+                if "visual" in k or (self.with_text and _is_text_key(k))}
         self.load_state_dict(synth.synth_state_dict(spec, seed), strict=False)
 
     def to(self, *a, **k):
@@ -117,6 +132,38 @@ class DaCLIP:
             ic = torch.nn.functional.normalize(ic, dim=-1)
             dc = torch.nn.functional.normalize(dc, dim=-1)
         return ic, dc
+
+    def encode_text(self, text: torch.Tensor, normalize: bool = False) -> torch.Tensor:
+        """daclip_model.py:125-126 -> CLIP.encode_text (model.py:237-249): token ids
+        [N, context_length] (open_clip.tokenize output) -> [N, embed_dim] fp32."""
+        if not self.with_text:
+            raise RuntimeError("DaCLIP built with with_text=False")
+        if not self._loaded:
+            raise RuntimeError("DaCLIP: weights not loaded")
+        tok = text.to(self.device, torch.int64).contiguous()
+        if tok.dim() != 2 or tok.shape[1] != self.text.context_length:
+            raise RuntimeError(f"expected [N,{self.text.context_length}] token ids, got {tuple(tok.shape)}")
+        out = torch.empty((tok.shape[0], self.vision.embed_dim), device=self.device, dtype=torch.float32)
+        h = self._h
+        with torch.cuda.device(self.device):
+            h.check(_lib.lib().dac_encode_text(h.h, _lib._ptr(tok), tok.shape[0], _lib._ptr(out), h.stream()),
+                    "encode_text")
+        return torch.nn.functional.normalize(out, dim=-1) if normalize else out
+
+    def degradation_probs(self, degra_features: torch.Tensor, text_features: torch.Tensor):
+        """evaluate_daclip.py:45-50, 78-84: probs = softmax(100 * d^ t^T) over the K class
+        texts and argmax (first maximum) -> (probs [B, K] fp32, argmax [B] int64)."""
+        d = degra_features.to(self.device, torch.float32).contiguous()
+        t = text_features.to(self.device, torch.float32).contiguous()
+        B, E = d.shape
+        K = t.shape[0]
+        probs = torch.empty((B, K), device=self.device, dtype=torch.float32)
+        am = torch.empty((B,), device=self.device, dtype=torch.int32)
+        h = self._h
+        with torch.cuda.device(self.device):
+            h.check(_lib.lib().dac_degradation_probs(h.h, _lib._ptr(d), _lib._ptr(t), B, K, E, _lib._ptr(probs),
+                                                     _lib._ptr(am), h.stream()), "degradation_probs")
+        return probs, am.long()
 
     def flops(self, B: int) -> float:
         return _lib.lib().dac_encode_flops(self._h.h, B)

@@ -11,6 +11,9 @@
  *       (load_network) and networks.py:10-15 (define_G -> ConditionalUNet(**setting)).
  *   dac_encode_image
  *       replaces DaCLIP.encode_image(image, control=True)   (open_clip/daclip_model.py:46-53)
+ *   dac_encode_text / dac_degradation_probs
+ *       replace DaCLIP.encode_text (daclip_model.py:125-126 -> model.py:237-249) and the
+ *       degradation-class scoring softmax(100 d^ t^T) -> argmax (evaluate_daclip.py:45-84)
  *   dac_unet_forward
  *       replaces the `sde.set_model(model)` callable: model(x, mu, t, text_context=,
  *       image_context=) -> noise (utils/sde_utils.py:163-164, 195-202;
@@ -65,6 +68,10 @@ typedef struct dac_config {
   int use_degra_context, use_image_context;
   int vit;
   int image_size, patch_size, width, layers, head_width, mlp_width, embed_dim;
+  /* Text tower (CLIPTextCfg, open_clip/model_configs/daclip_ViT-B-32.json text_cfg); needs vit.
+   * Zero `text` leaves it out (its checkpoint keys are then accepted and ignored). */
+  int text;
+  int context_length, vocab_size, text_width, text_heads, text_layers;
 } dac_config;
 
 int dac_create(int device, int dtype, const dac_config* cfg, dac_handle** out);
@@ -83,6 +90,18 @@ int dac_finalize_weights(dac_handle* h);
 /* img [B,3,S,S] (preprocessed, S = image_size) -> image_ctx [B,E], degra_ctx [B,E] fp32. */
 int dac_encode_image(dac_handle* h, const float* img, int B, float* image_ctx,
                      float* degra_ctx, void* stream);
+
+/* Text features (CLIP.encode_text, open_clip/model.py:237-249, via DaCLIP.encode_text
+ * daclip_model.py:125-126): tokens [N, context_length] int64 device ids (open_clip.tokenize
+ * output) -> text_features [N, embed_dim] fp32, unnormalised. Ids outside the vocabulary give
+ * NaN features (never an out-of-bounds read). */
+int dac_encode_text(dac_handle* h, const int64_t* tokens, int N, float* text_features, void* stream);
+
+/* Degradation-class scoring (evaluate_daclip.py:45-50, 78-84): probs[B][K] =
+ * softmax_k(100 * <degra_b / |degra_b|, text_k / |text_k|>), argmax[B] = first maximum.
+ * degra [B, E], text_features [K, E] fp32 device; K <= 64. */
+int dac_degradation_probs(dac_handle* h, const float* degra, const float* text_features, int B, int K,
+                          int E, float* probs, int32_t* argmax, void* stream);
 
 /* One ConditionalUNet forward: eps = model(xt, mu, t, text_ctx, image_ctx), all [B,3,H,W]
  * except contexts [B,context_dim]; text_ctx / image_ctx may be NULL. */

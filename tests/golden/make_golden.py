@@ -154,6 +154,49 @@ def gen_daclip():
                         image_context=ic.numpy(), degra_context=dc.numpy())
 
 
+DEGRADATIONS = ["motion-blurry", "hazy", "jpeg-compressed", "low-light", "noisy", "raindrop",
+                "rainy", "shadowed", "snowy", "uncompleted"]   # options/test.yml:4 order
+
+
+def text_images():
+    """The 6 encoder inputs of text_b32.npz (regenerated by the tests, not stored)."""
+    img = synth.synth_noise((6, 3, 224, 224), seed=31, tag="img4clip_text")
+    img[3:] = np.clip(img[3:] * 0.2 + synth.synth_images(3, 224, 224, seed=32), -3, 3)
+    return img
+
+
+def gen_text():
+    """Text tower + degradation-class scoring (daclip_model.py:125-126 -> model.py:237-249;
+    evaluate_daclip.py:45-50, 78-84): token ids from the reference tokenizer for the 10
+    class names, encode_text features, and softmax(100 d^ t^T) / argmax for 6 images."""
+    from open_clip import tokenize
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    tokens = tokenize(DEGRADATIONS)
+    tf = d.encode_text(tokens)
+    img = text_images()
+    _, dc = d.encode_image(T(img), control=True)
+    dn = dc / dc.norm(dim=-1, keepdim=True)
+    tn = tf / tf.norm(dim=-1, keepdim=True)
+    probs = (100.0 * dn @ tn.T).softmax(dim=-1)
+    extra = ["A photo of heavy rain!", "it's a JPEG-compressed image, isn't it?", "3x3 conv &amp; 512px",
+             "café  crème\tbrûlée", "low light " * 40]
+    np.savez_compressed(os.path.join(HERE, "text_b32.npz"), classes=np.array(DEGRADATIONS),
+                        extra_texts=np.array(extra), extra_tokens=tokenize(extra).numpy(),
+                        tokens=tokens.numpy(), text_features=tf.numpy(), degra=dc.numpy(),
+                        probs=probs.numpy(), argmax=probs.argmax(dim=-1).numpy())
+    small_v = dict(image_size=64, layers=3, width=128, patch_size=32)
+    small_t = dict(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+    d = _daclip(small_v, small_t, 64)
+    rng = np.random.default_rng(5)
+    tok = rng.integers(1, 62, size=(4, 16)).astype(np.int64)
+    for i, e in enumerate([3, 9, 15, 6]):                 # EOT (highest id) at varied positions
+        tok[i, e] = 63
+        tok[i, e + 1:] = 0
+    tf = d.encode_text(T(tok))
+    np.savez_compressed(os.path.join(HERE, "text_small.npz"), tokens=tok, text_features=tf.numpy())
+
+
 def gen_modules():
     """Per-module fixtures (small shapes) used to localise kernel bugs."""
     from models.modules.module_util import ResBlock, LinearAttention, default_conv, NonLinearity
@@ -190,9 +233,9 @@ def gen_img_metrics():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "modules", "img"]
+    which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "text", "modules", "img"]
     fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
-               modules=gen_modules, img=gen_img_metrics)
+               text=gen_text, modules=gen_modules, img=gen_img_metrics)
     for w in which:
         print("generating", w, flush=True)
         fns[w]()

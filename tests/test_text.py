@@ -1,0 +1,109 @@
+"""Text tower + degradation-class argmax: CLIP.encode_text
+(model.py:237-249 via daclip_model.py:125-126), the tokenizer (tokenizer.py:159-189) and the
+softmax(100 d^ t^T) scoring of evaluate_daclip.py:45-50, 78-84. Fixtures: tests/golden
+text_b32.npz / text_small.npz, made by running the reference (make_golden.py gen_text)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from daclip_amd import arch, synth
+
+REF_VOCAB = "/root/reference/universal-image-restoration/open_clip/bpe_simple_vocab_16e6.txt.gz"
+SMALL_V = dict(image_size=64, patch_size=32, width=128, layers=3, embed_dim=64)
+SMALL_T = dict(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+def text_images():
+    """The 6 encoder inputs of text_b32.npz (same recipe as make_golden.text_images)."""
+    img = synth.synth_noise((6, 3, 224, 224), seed=31, tag="img4clip_text")
+    img[3:] = np.clip(img[3:] * 0.2 + synth.synth_images(3, 224, 224, seed=32), -3, 3)
+    return img
+
+
+# ------------------------------------------------------------------ CPU: oracle + tokenizer
+def test_oracle_encode_text_matches_reference(golden):
+    from oracle import clip as OC
+    g = golden("text_small.npz")
+    sd = synth.synth_state_dict(arch.daclip_state_spec(arch.VisionConfig(**SMALL_V), arch.TextConfig(**SMALL_T)), 0)
+    assert rel(OC.encode_text(sd, g["tokens"], heads=2), g["text_features"]) < 1e-5
+    g = golden("text_b32.npz")
+    sd = synth.synth_state_dict(arch.daclip_state_spec(), 0)
+    assert rel(OC.encode_text(sd, g["tokens"], heads=8), g["text_features"]) < 1e-5
+    p = OC.degradation_probs(g["degra"], g["text_features"])
+    assert np.abs(p - g["probs"]).max() < 1e-5
+    assert np.array_equal(p.argmax(-1), g["argmax"])
+
+
+@pytest.mark.skipif(not os.path.exists(REF_VOCAB), reason="BPE vocabulary (reference data) not present")
+def test_tokenizer_matches_reference(golden):
+    from daclip_amd.tokenizer import tokenize
+    g = golden("text_b32.npz")
+    assert np.array_equal(tokenize(list(g["classes"]), vocab_path=REF_VOCAB).numpy(), g["tokens"])
+    assert np.array_equal(tokenize(list(g["extra_texts"]), vocab_path=REF_VOCAB).numpy(), g["extra_tokens"])
+
+
+def test_tokenizer_needs_vocab(monkeypatch):
+    from daclip_amd import tokenizer
+    monkeypatch.delenv("DACLIP_BPE_VOCAB", raising=False)
+    with pytest.raises(FileNotFoundError):
+        tokenizer.BPETokenizer(None)
+
+
+# ------------------------------------------------------------------ GPU: HIP path
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_encode_text_matches_reference(golden, dt):
+    from daclip_amd.open_clip import DaCLIP
+    tol = 1e-4 if dt == "fp32" else 5e-2
+    g = golden("text_small.npz")
+    m = DaCLIP(arch.VisionConfig(**SMALL_V), arch.TextConfig(**SMALL_T), dtype=dt)
+    m.load_synthetic(0)
+    tf = m.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
+    assert rel(tf, g["text_features"]) < tol
+    g = golden("text_b32.npz")
+    m = DaCLIP(dtype=dt)
+    m.load_synthetic(0)
+    tf = m.encode_text(torch.from_numpy(g["tokens"])).cpu().numpy()
+    assert rel(tf, g["text_features"]) < tol
+
+
+@pytest.mark.gpu
+def test_degradation_argmax_bit_exact(golden):
+    """Full chain on the HIP path in parity mode: encode_image(control=True) of 6 images,
+    encode_text of the 10 class names, softmax(100 d^ t^T) -> argmax equal to the
+    reference's (and the top-3 ranking), probabilities within 1e-4."""
+    from daclip_amd.open_clip import DaCLIP
+    g = golden("text_b32.npz")
+    m = DaCLIP(dtype="fp32")
+    m.load_synthetic(0)
+    _, dc = m.encode_image(torch.from_numpy(text_images()).cuda(), control=True)
+    tf = m.encode_text(torch.from_numpy(g["tokens"]))
+    probs, am = m.degradation_probs(dc, tf)
+    probs = probs.cpu().numpy()
+    assert np.array_equal(am.cpu().numpy(), g["argmax"])
+    assert np.array_equal(np.argsort(-probs, 1)[:, :3], np.argsort(-g["probs"], 1)[:, :3])
+    assert np.abs(probs - g["probs"]).max() < 1e-4
+    # bf16 (perf) path: same classes.
+    mb = DaCLIP(dtype="bf16")
+    mb.load_synthetic(0)
+    _, dcb = mb.encode_image(torch.from_numpy(text_images()).cuda(), control=True)
+    _, amb = mb.degradation_probs(dcb, mb.encode_text(torch.from_numpy(g["tokens"])))
+    assert np.array_equal(amb.cpu().numpy(), g["argmax"])
+
+
+@pytest.mark.gpu
+def test_encode_text_bad_ids_give_nan_not_fault(golden):
+    from daclip_amd.open_clip import DaCLIP
+    m = DaCLIP(arch.VisionConfig(**SMALL_V), arch.TextConfig(**SMALL_T), dtype="fp32")
+    m.load_synthetic(0)
+    tok = torch.from_numpy(golden("text_small.npz")["tokens"]).clone()
+    tok[1, 2] = 10_000                                    # outside the 64-entry vocabulary
+    tf = m.encode_text(tok).cpu()
+    assert torch.isnan(tf[1]).all() and torch.isfinite(tf[0]).all()
