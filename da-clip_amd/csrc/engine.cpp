@@ -286,6 +286,9 @@ struct UNetNet {
   const float *tm1w, *tm1b, *tm3w, *tm3b, *prompt = nullptr, *t0w = nullptr, *t0b = nullptr,
               *t2w = nullptr, *t2b = nullptr, *pmw = nullptr, *pmb = nullptr;
   std::vector<Level> downs, ups;
+  ConvW half_down, half_up;            // Wild-IR scale 0.5 wrap (downsample / upsample.1)
+  bool half = false;
+  int st_from = 3;
   RB mid1, mid2, fin;
   Attn mid_attn;
   int ss_total = 0, cc_total = 0, n_st = 0;
@@ -294,6 +297,8 @@ struct UNetNet {
     nf = c.nf; depth = c.depth; tdim = nf * 4; ctx = c.context_dim;
     degra = ctx > 0 && c.use_degra_context;
     imgctx = ctx > 0 && c.use_image_context;
+    half = c.unet_scale_half != 0;
+    st_from = c.unet_st_from > 0 ? c.unet_st_from : 3;
     std::vector<int> m = {1};
     for (int i = 0; i < depth; ++i) m.push_back(c.ch_mult[i]);
     for (int i = 0; i < depth; ++i) levels.push_back({nf * m[i], nf * m[i + 1]});
@@ -361,6 +366,10 @@ struct UNetNet {
     ss_total = cc_total = n_st = 0;
     if (degra) prompt = P.f32("prompt", {1, tdim});
     init_conv = P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7);
+    if (half) {
+      half_down = P.conv("downsample.weight", nf, nf, 4, 4, "downsample.bias");
+      half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias");
+    }
     tm1w = P.f32("time_mlp.1.weight", {tdim, nf});
     tm1b = P.f32("time_mlp.1.bias", {tdim});
     tm3w = P.f32("time_mlp.3.weight", {tdim, tdim});
@@ -381,7 +390,7 @@ struct UNetNet {
       Level& L = downs[i];
       L.b1 = load_rb(P, p + "0.", din, din);
       L.b2 = load_rb(P, p + "1.", din, din);
-      L.at = load_attn(P, p + "2.", din, imgctx && i >= 3);
+      L.at = load_attn(P, p + "2.", din, imgctx && i >= st_from);
       L.samp = i != depth - 1 ? P.conv(p + "3.weight", dout, din, 4, 4, p + "3.bias")
                               : P.conv(p + "3.weight", dout, din, 3, 3);
     }
@@ -392,7 +401,7 @@ struct UNetNet {
       Level& L = ups[j];
       L.b1 = load_rb(P, p + "0.", dout + din, dout);
       L.b2 = load_rb(P, p + "1.", dout + din, dout);
-      L.at = load_attn(P, p + "2.", dout, imgctx && i >= 3);
+      L.at = load_attn(P, p + "2.", dout, imgctx && i >= st_from);
       L.samp = i != 0 ? P.conv(p + "3.1.weight", din, dout, 3, 3, p + "3.1.bias")
                       : P.conv(p + "3.weight", din, dout, 3, 3);
     }
@@ -578,6 +587,12 @@ struct UNetNet {
     std::vector<std::pair<const void*, int>> hs;
     const void* cur = x0;
     int h = Hp, w = Wp;
+    if (half) {                                   // Wild-IR: levels run at half resolution
+      T* xd = r.alloc<T>((size_t)B * (Hp / 2) * (Wp / 2) * nf);
+      conv_call<T>(r, half_down, x0, nf, nf, nullptr, 0, B, Hp, Wp, 0, 2, 1, xd, nf, Epi());
+      cur = xd;
+      h = Hp / 2; w = Wp / 2;
+    }
     for (int i = 0; i < depth; ++i) {
       const auto [din, dout] = levels[i];
       Level& L = downs[i];
@@ -620,6 +635,12 @@ struct UNetNet {
         conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 0, 1, 1, y, din, Epi());
         cur = y;
       }
+    }
+    if (half) {
+      T* xu = r.alloc<T>((size_t)B * Hp * Wp * nf);
+      conv_call<T>(r, half_up, cur, nf, nf, nullptr, 0, B, h, w, 1, 1, 1, xu, nf, Epi());
+      cur = xu;
+      h = Hp; w = Wp;
     }
     cur = resblock(r, fin, cur, nf, x0, nf, B, h, w, ss);
     conv_call<T>(r, final_conv, cur, nf, nf, nullptr, 0, B, h, w, 0, 1, 1, out, ldo, Epi());

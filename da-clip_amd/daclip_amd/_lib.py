@@ -39,7 +39,8 @@ class DacConfig(ctypes.Structure):
                 ("width", ctypes.c_int), ("layers", ctypes.c_int), ("head_width", ctypes.c_int),
                 ("mlp_width", ctypes.c_int), ("embed_dim", ctypes.c_int),
                 ("text", ctypes.c_int), ("context_length", ctypes.c_int), ("vocab_size", ctypes.c_int),
-                ("text_width", ctypes.c_int), ("text_heads", ctypes.c_int), ("text_layers", ctypes.c_int)]
+                ("text_width", ctypes.c_int), ("text_heads", ctypes.c_int), ("text_layers", ctypes.c_int),
+                ("unet_scale_half", ctypes.c_int), ("unet_st_from", ctypes.c_int)]
 
 
 _lib = None

@@ -30,6 +30,11 @@ class UNetConfig:
     context_dim: int = 512
     use_degra_context: bool = True
     use_image_context: bool = True
+    # Wild-IR (config/wild-ir/models/modules/DenoisingUNet_arch.py:22-40, 136-140, 176-180):
+    # scale == 0.5 adds Downsample(nf, nf) after init_conv and Upsample(nf, nf) before the
+    # final concat; SpatialTransformer levels start at depth - 1 there, at 3 in daclip-sde.
+    scale: float = 1.0
+    st_from: int = 3
 
     @property
     def depth(self) -> int:
@@ -46,7 +51,7 @@ class UNetConfig:
 
     def uses_transformer(self, level: int) -> bool:
         """SpatialTransformer vs LinearAttention selection, DenoisingUNet_arch.py:78-83."""
-        return self.use_image_context and self.context_dim > 0 and level >= 3
+        return self.use_image_context and self.context_dim > 0 and level >= self.st_from
 
 
 @dataclass(frozen=True)
@@ -158,6 +163,11 @@ def unet_state_spec(cfg: UNetConfig = UNetConfig()) -> "OrderedDict[str, Shape]"
     if cfg.context_dim > 0 and cfg.use_degra_context:
         sd["prompt"] = (1, td)
     sd["init_conv.weight"] = (nf, cfg.in_nc * 2, 7, 7)
+    if cfg.scale == 0.5:
+        sd["downsample.weight"] = (nf, nf, 4, 4)
+        sd["downsample.bias"] = (nf,)
+        sd["upsample.1.weight"] = (nf, nf, 3, 3)
+        sd["upsample.1.bias"] = (nf,)
     sd["time_mlp.1.weight"] = (td, nf)
     sd["time_mlp.1.bias"] = (td,)
     sd["time_mlp.3.weight"] = (td, td)
@@ -199,6 +209,11 @@ def unet_state_spec(cfg: UNetConfig = UNetConfig()) -> "OrderedDict[str, Shape]"
     sd["final_conv.weight"] = (cfg.out_nc, nf, 3, 3)
     sd["final_conv.bias"] = (cfg.out_nc,)
     return sd
+
+
+# Wild-IR network_G.setting (config/wild-ir/options/inference.yml:30-39).
+WILD_IR_UNET = UNetConfig(context_dim=768, use_degra_context=False, use_image_context=True,
+                          scale=0.5, st_from=3)
 
 
 # ----------------------------------------------------------------------------- DaCLIP

@@ -74,3 +74,35 @@ def calculate_psnr(img1, img2):
     if mse == 0:
         return float("inf")
     return 20 * math.log10(255.0 / math.sqrt(mse))
+
+
+def make_grid(tensor: torch.Tensor, nrow: int = 8, padding: int = 2, pad_value: float = 0.0) -> torch.Tensor:
+    """torchvision.utils.make_grid (normalize=False) for [B,C,H,W] -> [C, H', W'] (host)."""
+    t = tensor.detach().float().cpu()
+    if t.dim() == 3:
+        t = t.unsqueeze(0)
+    if t.size(1) == 1:
+        t = torch.cat((t, t, t), 1)
+    if t.size(0) == 1:
+        return t.squeeze(0)
+    n = t.size(0)
+    xm = min(nrow, n)
+    ym = (n + xm - 1) // xm
+    h, w = t.size(2) + padding, t.size(3) + padding
+    grid = torch.full((t.size(1), h * ym + padding, w * xm + padding), pad_value)
+    k = 0
+    for y in range(ym):
+        for x in range(xm):
+            if k >= n:
+                break
+            grid[:, y * h + padding:(y + 1) * h, x * w + padding:(x + 1) * w] = t[k]
+            k += 1
+    return grid
+
+
+def save_image(tensor: torch.Tensor, fp: str, nrow: int = 8, padding: int = 2) -> None:
+    """torchvision.utils.save_image(normalize=False): grid * 255 + 0.5, clamp, uint8 PNG."""
+    grid = make_grid(tensor, nrow=nrow, padding=padding)
+    arr = grid.mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
+    Image.fromarray(arr).save(fp)
+

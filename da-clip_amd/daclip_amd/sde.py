@@ -10,11 +10,13 @@ library kernel (dac_posterior_step).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
 
 from . import _lib
+from .preprocess import save_image
 from .unet import ConditionalUNet
 
 
@@ -102,10 +104,21 @@ class IRSDE:
     def _native(self):
         return self.model if isinstance(self.model, ConditionalUNet) else None
 
-    def _loop(self, mode, xt, T, noises, **kwargs):
+    def _save_state(self, x, t, save_dir):
+        """sde_utils.py:269-275 / 305-311 verbatim semantics: every T // 100 steps (T < 100 makes
+        the interval 0 and raises, as in the reference), channel halves side by side (an odd
+        channel count fails in torch.cat exactly like the reference), save_image PNG."""
+        interval = self.T // 100
+        if t % interval == 0:
+            idx = t // interval
+            os.makedirs(save_dir, exist_ok=True)
+            x_l, x_r = x.detach().cpu().chunk(2, dim=1)
+            save_image(torch.cat([x_l, x_r], dim=3), f"{save_dir}/state_{idx}.png")
+
+    def _loop(self, mode, xt, T, noises, save_states=False, save_dir="state", **kwargs):
         m = self._native()
         mu = self.mu if isinstance(self.mu, torch.Tensor) else torch.full_like(xt, float(self.mu))
-        if m is not None:
+        if m is not None and not save_states:
             h = m._h
             dev = m.device
             x = xt.to(dev, torch.float32).contiguous().clone()
@@ -129,12 +142,15 @@ class IRSDE:
                                                    _lib._ptr(nz), self.seed, h.stream()),
                         "sde_reverse")
             return x
-        # Generic callable model: the reference's loop (sde_utils.py:297-313 / 261-277).
+        # Generic callable model (or save_states): the reference's per-step loop
+        # (sde_utils.py:297-313 / 261-277) with the native sampler update.
         x = xt.clone().float()
         for i, t in enumerate(range(T, 0, -1)):
             eps = self.noise_fn(x, t, self.sample_scale, **kwargs).float().contiguous()
             z = noises[i] if noises is not None else torch.randn_like(x)
             x = self.step(mode, x, eps, mu, z, t)
+            if save_states:
+                self._save_state(x, t, save_dir)
         return x
 
     def step(self, mode, x, eps, mu, z, t):
@@ -159,8 +175,8 @@ class IRSDE:
     def reverse_posterior(self, xt, T=-1, save_states=False, save_dir="posterior_state",
                           noises=None, **kwargs):
         T = self.sample_T if T < 0 else T
-        return self._loop(_lib.DAC_POSTERIOR, xt, T, noises, **kwargs)
+        return self._loop(_lib.DAC_POSTERIOR, xt, T, noises, save_states, save_dir, **kwargs)
 
     def reverse_sde(self, xt, T=-1, save_states=False, save_dir="sde_state", noises=None, **kwargs):
         T = self.sample_T if T < 0 else T
-        return self._loop(_lib.DAC_SDE, xt, T, noises, **kwargs)
+        return self._loop(_lib.DAC_SDE, xt, T, noises, save_states, save_dir, **kwargs)

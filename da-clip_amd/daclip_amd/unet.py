@@ -26,6 +26,10 @@ def unet_config(cfg: arch.UNetConfig) -> _lib.DacConfig:
     c.context_dim = cfg.context_dim if cfg.context_dim is not None else -1
     c.use_degra_context = int(cfg.use_degra_context)
     c.use_image_context = int(cfg.use_image_context)
+    if cfg.scale not in (1, 0.5):
+        raise ValueError(f"scale {cfg.scale}: only 1 and 0.5 exist in the reference")
+    c.unet_scale_half = int(cfg.scale == 0.5)
+    c.unet_st_from = cfg.st_from
     return c
 
 
@@ -36,10 +40,14 @@ def _incompatible(expected: Sequence[str], got: Sequence[str]):
 
 class ConditionalUNet:
     def __init__(self, in_nc=3, out_nc=3, nf=64, ch_mult=(1, 2, 4, 4), context_dim=512,
-                 use_degra_context=True, use_image_context=False, upscale=1,
+                 use_degra_context=True, use_image_context=False, upscale=1, scale=1,
                  device="cuda", dtype="fp32"):
+        """daclip-sde signature (`upscale`, unused there) plus the Wild-IR `scale` (0.5 adds the
+        half-resolution wrap, config/wild-ir/models/modules/DenoisingUNet_arch.py:22-40)."""
+        depth = len(ch_mult)
         self.cfg = arch.UNetConfig(in_nc, out_nc, nf, tuple(ch_mult), context_dim,
-                                   bool(use_degra_context), bool(use_image_context))
+                                   bool(use_degra_context), bool(use_image_context),
+                                   scale=scale, st_from=depth - 1 if scale != 1 else 3)
         self.depth = self.cfg.depth
         self.upscale = upscale
         self.dtype = dtype

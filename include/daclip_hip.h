@@ -72,6 +72,10 @@ typedef struct dac_config {
    * Zero `text` leaves it out (its checkpoint keys are then accepted and ignored). */
   int text;
   int context_length, vocab_size, text_width, text_heads, text_layers;
+  /* Wild-IR UNet variant (config/wild-ir/models/modules/DenoisingUNet_arch.py:22-40):
+   * unet_scale_half = 1 for `scale: 0.5` (extra Downsample/Upsample around the levels);
+   * unet_st_from = first level with a SpatialTransformer (0 = 3, the daclip-sde rule). */
+  int unet_scale_half, unet_st_from;
 } dac_config;
 
 int dac_create(int device, int dtype, const dac_config* cfg, dac_handle** out);

@@ -112,7 +112,8 @@ def time_embedding(sd, t, nf, text_context=None):
 
 
 def forward(sd, xt, cond, time, text_context=None, image_context=None, depth=4):
-    """ConditionalUNet.forward (DenoisingUNet_arch.py:118-174)."""
+    """ConditionalUNet.forward (DenoisingUNet_arch.py:118-174; the Wild-IR variant's half-scale
+    wrap, config/wild-ir/models/modules/DenoisingUNet_arch.py:122-189, is keyed on its weights)."""
     nf = sd["init_conv.weight"].shape[0]
     x = np.concatenate([xt - cond, cond], 1).astype(f32)
     H, W = x.shape[2:]
@@ -120,6 +121,8 @@ def forward(sd, xt, cond, time, text_context=None, image_context=None, depth=4):
     x = F.reflect_pad(x, (s - H % s) % s, (s - W % s) % s)
     x = F.conv2d(x, sd["init_conv.weight"], pad=3)
     x_ = x.copy()
+    if "downsample.weight" in sd:                # Wild-IR scale 0.5 (wild-ir arch :136-140)
+        x = F.conv2d(x, sd["downsample.weight"], sd["downsample.bias"], stride=2, pad=1)
     t = time_embedding(sd, time, nf, text_context)
     ctx = image_context[:, None, :] if image_context is not None else None
 
@@ -149,6 +152,8 @@ def forward(sd, xt, cond, time, text_context=None, image_context=None, depth=4):
             x = F.conv2d(F.upsample_nearest2x(x), sd[p + "3.1.weight"], sd[p + "3.1.bias"], pad=1)
         else:
             x = F.conv2d(x, sd[p + "3.weight"], pad=1)
+    if "upsample.1.weight" in sd:                # wild-ir arch :176-180
+        x = F.conv2d(F.upsample_nearest2x(x), sd["upsample.1.weight"], sd["upsample.1.bias"], pad=1)
     x = np.concatenate([x, x_], 1)
     x = resblock(sd, "final_res_block.", x, t)
     x = F.conv2d(x, sd["final_conv.weight"], sd["final_conv.bias"], pad=1)

@@ -64,3 +64,18 @@ def import_reference():
     import open_clip  # noqa: E402
     import utils as ref_utils  # noqa: E402
     return ConditionalUNet, open_clip, ref_utils
+
+
+def import_wild_unet():
+    """The Wild-IR ConditionalUNet (config/wild-ir/models/modules/DenoisingUNet_arch.py), loaded
+    inside the daclip-sde `models.modules` package: its module_util / attention imports resolve
+    to daclip-sde's files, which are identical for every class the network uses."""
+    import importlib.util
+    import_reference()
+    path = REF + "/config/wild-ir/models/modules/DenoisingUNet_arch.py"
+    spec = importlib.util.spec_from_file_location("models.modules.DenoisingUNet_arch_wild", path)
+    mod = importlib.util.module_from_spec(spec)
+    mod.__package__ = "models.modules"
+    spec.loader.exec_module(mod)
+    return mod.ConditionalUNet
+

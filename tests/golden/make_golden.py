@@ -197,6 +197,36 @@ def gen_text():
     np.savez_compressed(os.path.join(HERE, "text_small.npz"), tokens=tok, text_features=tf.numpy())
 
 
+def wild_images():
+    """Encoder input of wild_l14_encode.npz (regenerated by the tests, not stored)."""
+    return synth.synth_noise((1, 3, 224, 224), seed=41, tag="img4clip_wild")
+
+
+def gen_wild():
+    """Wild-IR (BASELINE config 4 model): ConditionalUNet(scale=0.5, context 768, image context
+    only; config/wild-ir/options/inference.yml:30-39) forwards and the ViT-L/14 DaCLIP
+    encode_image(control=True) (wild-daclip_ViT-L-14, inference.py:68-96)."""
+    WildUNet = _refimport.import_wild_unet()
+    setting = dict(in_nc=3, out_nc=3, nf=64, ch_mult=[1, 2, 4, 8], context_dim=768,
+                   use_degra_context=False, use_image_context=True, scale=0.5)
+    m = WildUNet(**setting).eval()
+    spec = load(m, seed=0)
+    json.dump({k: list(v) for k, v in spec.items()}, open(os.path.join(HERE, "wild_state_spec.json"), "w"))
+    out = {}
+    for tag, (B, H, W) in (("32x32", (1, 32, 32)), ("48x40", (2, 48, 40))):
+        xt = synth.synth_noise((B, 3, H, W), seed=51, tag="wx" + tag) * 0.3 + 0.5
+        mu = synth.synth_images(B, H, W, seed=52)
+        ic = synth.synth_noise((B, 768), seed=53, tag="wic" + tag)
+        out[f"{tag}_xt"], out[f"{tag}_mu"], out[f"{tag}_ic"] = xt, mu, ic
+        out[f"{tag}_out"] = m(T(xt), T(mu), 37.0, image_context=T(ic)).numpy()
+    np.savez_compressed(os.path.join(HERE, "wild_unet_fwd.npz"), **out)
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-L-14.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    ic, dc = d.encode_image(T(wild_images()), control=True)
+    np.savez_compressed(os.path.join(HERE, "wild_l14_encode.npz"), image_context=ic.numpy(),
+                        degra_context=dc.numpy())
+
+
 def gen_modules():
     """Per-module fixtures (small shapes) used to localise kernel bugs."""
     from models.modules.module_util import ResBlock, LinearAttention, default_conv, NonLinearity
@@ -233,9 +263,9 @@ def gen_img_metrics():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "text", "modules", "img"]
+    which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "text", "wild", "modules", "img"]
     fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
-               text=gen_text, modules=gen_modules, img=gen_img_metrics)
+               text=gen_text, wild=gen_wild, modules=gen_modules, img=gen_img_metrics)
     for w in which:
         print("generating", w, flush=True)
         fns[w]()

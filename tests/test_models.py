@@ -89,3 +89,39 @@ def test_predictor_batch_matches_manual_pipeline():
     res = p.sde.reverse_posterior(noisy.cuda(), text_context=dc.float(), image_context=ic.float())
     for i in range(2):
         assert np.array_equal(out[i], tensor2img(res[i].cpu()))
+
+
+def test_make_grid_matches_torchvision_layout():
+    from daclip_amd.preprocess import make_grid
+    t = torch.arange(3 * 2 * 2 * 3, dtype=torch.float32).reshape(3, 2, 2, 3)
+    t = torch.cat([t, t[:, :1]], 1)                      # 3 channels
+    g = make_grid(t, nrow=2, padding=1)
+    assert g.shape == (3, 2 * 3 + 1, 2 * 4 + 1)
+    assert torch.equal(g[:, 1:3, 1:4], t[0]) and torch.equal(g[:, 1:3, 5:8], t[1])
+    assert torch.equal(g[:, 4:6, 1:4], t[2]) and float(g[:, 4:6, 5:8].abs().sum()) == 0.0
+    assert torch.equal(make_grid(t[:1]), t[0])
+
+
+@pytest.mark.gpu
+def test_save_states_semantics(tmp_path):
+    """sde_utils.py:305-311: a state PNG every T//100 steps (channel halves side by side);
+    3-channel states fail in torch.cat like the reference; T < 100 -> interval 0 raises."""
+    from daclip_amd.sde import IRSDE
+    from PIL import Image
+    s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+    x6 = torch.rand(1, 6, 8, 8, device="cuda")
+    s.set_mu(torch.rand(1, 6, 8, 8, device="cuda"))
+    s.set_model(lambda x, mu, t, **k: 0.1 * (x - mu))
+    s.reverse_posterior(x6, T=3, save_states=True, save_dir=str(tmp_path / "st"))
+    files = sorted(p.name for p in (tmp_path / "st").iterdir())
+    assert files == ["state_1.png", "state_2.png", "state_3.png"]
+    assert Image.open(tmp_path / "st" / "state_1.png").size == (16, 8)
+    s.set_mu(torch.rand(1, 3, 8, 8, device="cuda"))
+    with pytest.raises(RuntimeError):
+        s.reverse_posterior(torch.rand(1, 3, 8, 8, device="cuda"), T=2, save_states=True,
+                            save_dir=str(tmp_path / "st3"))
+    s10 = IRSDE(max_sigma=50, T=10, schedule="cosine", eps=0.005)
+    s10.set_mu(torch.rand(1, 6, 8, 8, device="cuda"))
+    s10.set_model(lambda x, mu, t, **k: 0.1 * x)
+    with pytest.raises(ZeroDivisionError):
+        s10.reverse_posterior(x6, T=2, save_states=True, save_dir=str(tmp_path / "s10"))

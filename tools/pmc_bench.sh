@@ -14,7 +14,7 @@ for P in "FETCH_SIZE GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES" \
   # Per-dispatch counters do not depend on T (every step runs the same kernels on the same
   # shapes), so T=10 keeps the serialized PMC run short.
   DAC_NO_GRAPH=1 timeout -s KILL 600 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_$TAG/p$i -o run -- \
-    python -u bench.py --steps 1 --warmup 0 --T 10 --no-cpu-baseline --no-roofline ${BENCH_ARGS} \
+    python -u bench.py --steps 1 --warmup 0 --T 10 --no-cpu-baseline --no-roofline --no-psnr ${BENCH_ARGS} \
     > gpurun_out/pmc_$TAG/p$i.log 2>&1 &
   pid=$!
   while kill -0 $pid 2>/dev/null; do sleep 20; echo "pass $i $(date +%T)" >> gpurun_out/pmc_$TAG/heartbeat; done
