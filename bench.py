@@ -49,8 +49,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--batch", type=int, default=8, help="images per GPU")
-    p.add_argument("--res", type=int, default=256)
+    p.add_argument("--model", default="universal-ir", choices=["universal-ir", "wild-ir"],
+                   help="universal-ir: ViT-B/32 DA-CLIP + UIR UNet (BASELINE configs[1]); wild-ir: "
+                        "ViT-L/14 + scale-0.5 UNet (configs[3], default 512^2, 2 images per GPU)")
+    p.add_argument("--batch", type=int, default=None, help="images per GPU (8; wild-ir 2)")
+    p.add_argument("--res", type=int, default=None, help="resolution (256; wild-ir 512)")
     p.add_argument("--T", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--kernel-id", type=int, default=306,
@@ -59,7 +62,21 @@ def parse():
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the bf16-vs-fp32 PSNR sample")
     p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")
-    return p.parse_args()
+    a = p.parse_args()
+    wild = a.model == "wild-ir"
+    a.batch = a.batch or (2 if wild else 8)
+    a.res = a.res or (512 if wild else 256)
+    return a
+
+
+def model_setup(args):
+    """(UNet config, UNet ctor kwargs, vision cfg, text cfg) of the benchmarked model."""
+    from daclip_amd import arch
+    if args.model == "wild-ir":
+        return (arch.WILD_IR_UNET, dict(context_dim=768, use_degra_context=False, use_image_context=True,
+                                        scale=0.5), arch.VIT_L_14, arch.TEXT_L_14)
+    return arch.UNetConfig(), dict(context_dim=512, use_degra_context=True, use_image_context=True), \
+        arch.VIT_B_32, arch.TEXT_B_32
 
 
 def setup_dist(args):
@@ -111,7 +128,7 @@ def psnr_sample(args, wu_keys, clip, unet_bf16, lq, img, dev):
     from daclip_amd.sde import IRSDE
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     t0 = time.perf_counter()
-    u32 = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype="fp32")
+    u32 = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], **model_setup(args)[1], device=dev, dtype="fp32")
     u32.load_state_dict(synth.synth_state_dict(wu_keys, 0))
     ic, dc = clip.encode_image(img, control=True)
     R = lq.shape[-1]
@@ -140,17 +157,18 @@ def main():
     from daclip_amd.open_clip import DaCLIP
     from daclip_amd.sde import IRSDE
 
-    ucfg = arch.UNetConfig()
+    ucfg, ukw, vcfg, tcfg = model_setup(args)
     uspec = arch.unet_state_spec(ucfg)
-    cspec = {k: s for k, s in arch.daclip_state_spec().items() if k.startswith(("clip.visual.", "visual_control."))}
+    cspec = {k: s for k, s in arch.daclip_state_spec(vcfg, tcfg).items()
+             if k.startswith(("clip.visual.", "visual_control."))}
     sd_u = synth.synth_state_dict(uspec, 0) if rank == 0 else None
     sd_c = synth.synth_state_dict(cspec, 0) if rank == 0 else None
     wu = shard.broadcast_state(sd_u, list(uspec), dev)
     wc = shard.broadcast_state(sd_c, list(cspec), dev)
 
-    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype=args.dtype)
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], **ukw, device=dev, dtype=args.dtype)
     unet.load_state_dict(wu)
-    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, device=dev, dtype=args.dtype, with_text=False)
+    clip = DaCLIP(vcfg, tcfg, device=dev, dtype=args.dtype, with_text=False)
     clip.load_state_dict(wc, strict=False)
     del wu, wc
     sde = IRSDE(max_sigma=50, T=args.T, schedule="cosine", eps=0.005)
@@ -225,7 +243,9 @@ def main():
         images = n_glob * args.steps
         ach = fl.value / (mean_ms.value * 1e-3) / 1e12 if n_launch > 0 else None
         roof = None
-        pmc = pmc_entry(args.kernel_id, args.dtype)
+        # The committed PMC passes were collected on the default workload only.
+        default_wl = args.model == "universal-ir" and args.batch == 8 and args.res == 256
+        pmc = pmc_entry(args.kernel_id, args.dtype) if default_wl else None
         if n_launch > 0:
             roof = {"kernel": f"conv_kernel class {args.kernel_id} (3x3 implicit-GEMM, {args.dtype})",
                     "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_PEAK[args.dtype],
@@ -244,12 +264,18 @@ def main():
         uflops = unet.flops(B, R, R)
         eflops = clip.flops(B)
         total_tf = (args.T * uflops + eflops) / B / 1e12
-        res = {"metric": METRIC, "value": round(images / el, 4), "unit": "images/s", "n_gpus": ws,
+        wild = args.model == "wild-ir"
+        metric = METRIC if not wild else METRIC.replace("@256x256", f"@{R}x{R} (Wild-IR)")
+        res = {"metric": metric, "value": round(images / el, 4), "unit": "images/s", "n_gpus": ws,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 2),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-               "data": "synthetic (random-init ViT-B/32 DA-CLIP + nf=64 ConditionalUNet, synthetic LQ)",
-               "config": {"workload": f"deraining-shaped synthetic batch, {R}x{R}, batch={B}/GPU, "
-                                      f"{args.T} IR-SDE posterior steps, hipGraph loop (BASELINE configs[1])",
+               "data": ("synthetic (random-init ViT-L/14 DA-CLIP + Wild-IR scale-0.5 ConditionalUNet, synthetic LQ)"
+                        if wild else "synthetic (random-init ViT-B/32 DA-CLIP + nf=64 ConditionalUNet, synthetic LQ)"),
+               "config": {"workload": (f"Wild-IR synthetic batch, {R}x{R}, batch={B}/GPU, {args.T} IR-SDE "
+                                       f"posterior steps, hipGraph loop (BASELINE configs[3])") if wild else
+                                      (f"deraining-shaped synthetic batch, {R}x{R}, batch={B}/GPU, "
+                                       f"{args.T} IR-SDE posterior steps, hipGraph loop (BASELINE configs[1])"),
+                          "model": args.model,
                           "batch_per_gpu": B, "global_batch": n_glob, "resolution": R, "sde_steps": args.T,
                           "sampler": "posterior", "parallelism": f"dp{ws}"},
                "model_tflop_per_image": round(total_tf, 3),
