@@ -258,8 +258,12 @@ def gen_img_metrics():
     b = np.clip(a + 0.03 * synth.synth_noise(a.shape, seed=22, tag="pert"), -0.1, 1.1)
     ua = ref_utils.tensor2img(T(a.copy()))
     ub = ref_utils.tensor2img(T(b.copy()))
+    from data.util import bgr2ycbcr          # data/util.py:189-210 (no cv2 call on this path)
+    fa = ua.astype(np.float64) / 255.0
     np.savez_compressed(os.path.join(HERE, "img_metrics.npz"), a=a, b=b, ua=ua, ub=ub,
-                        psnr=np.float64(ref_utils.calculate_psnr(ua, ub)))
+                        psnr=np.float64(ref_utils.calculate_psnr(ua, ub)),
+                        y_u8=bgr2ycbcr(ua.copy(), only_y=True), ycc_u8=bgr2ycbcr(ua.copy(), only_y=False),
+                        y_f=bgr2ycbcr(fa.copy(), only_y=True), ycc_f=bgr2ycbcr(fa.copy(), only_y=False))
 
 
 if __name__ == "__main__":
