@@ -38,3 +38,20 @@ def test_create_without_gpu_fails_cleanly():
         pytest.skip("CPU-only check")
     with pytest.raises(RuntimeError, match="GPU"):
         _lib.Handle(torch.device("cuda", 0), "fp32", _lib.DacConfig())
+
+
+def test_config_struct_matches_header():
+    """daclip_amd._lib.DacConfig must list dac_config's fields in header order (the library
+    reads the whole struct)."""
+    from daclip_amd import _lib
+    src = open(os.path.join(ROOT, "include", "daclip_hip.h")).read()
+    body = re.search(r"typedef struct dac_config \{(.*?)\} dac_config;", src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        assert decl.startswith("int "), decl
+        names += [re.sub(r"\[.*\]", "", n).strip() for n in decl[4:].split(",")]
+    assert [f[0] for f in _lib.DacConfig._fields_] == names
