@@ -27,6 +27,8 @@ HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
+    (312, "bf16"): "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi3EEEvNS_8ConvArgsEi",
+    (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi3EEEvNS_8ConvArgsEi",
     (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (306, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
@@ -56,8 +58,8 @@ def parse():
     p.add_argument("--res", type=int, default=None, help="resolution (256; wild-ir 512)")
     p.add_argument("--T", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--kernel-id", type=int, default=306,
-                   help="conv class timed for the roofline (kh*100 + variant; 306 = 3x3 row-halo, Cout<=64)")
+    p.add_argument("--kernel-id", type=int, default=312,
+                   help="conv class timed for the roofline (kh*100 + variant; 312 = 3x3 interleaved-row v4 tiles)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the bf16-vs-fp32 PSNR sample")

@@ -11,6 +11,7 @@
 typedef __bf16 bf16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define DEV __device__ __forceinline__
@@ -76,6 +77,21 @@ template <> struct Mma<float> {
 
 DEV float silu_f(float x) { return x / (1.f + expf(-x)); }
 DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// Exact-form GELU 0.5 x (1 + erf(x / sqrt 2)) with erf from Abramowitz & Stegun 7.1.26
+// (|error| <= 1.5e-7): 1 + erf is formed as 2 - q or q, q = erfc(|z|) = t P(t) exp(-z^2), so
+// the negative tail has no cancellation. About 12 instructions against ~30 for erff; used by
+// the GEMM epilogues (GEGLU, ViT MLP), where erff dominated the epilogue.
+DEV float gelu_fast(float x) {
+  // No FP contraction: the value must not depend on the inlining context (an epilogue's fast
+  // and general paths must agree bit for bit, or results depend on batch composition).
+#pragma clang fp contract(off)
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __frcp_rn(fmaf(0.3275911f, z, 1.f));
+  const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
+                                   -0.284496736f), 0.254829592f);
+  const float q = p * __expf(-z * z);
+  return 0.5f * x * (x >= 0.f ? 2.f - q : q);
+}
 
 DEV float wave_sum(float v) {
 #pragma unroll

@@ -5,13 +5,20 @@
 
 namespace dac {
 
+int g_conv3_force = -1;
+int g_conv2_force = 0;
+extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
+extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }
+
 template <typename T, int KH, int KW, int S, int P>
 void conv_dispatch(const ConvArgs& a, hipStream_t st);
 
 // Kernel variant conv_dispatch selects (mirrors its logic); used to label timed launches:
 // 0/1/2 = v1 256x16 / 256x64 / 128x128, 3/4/5 = v2 256x64 / 256x128 / 128x128,
 // 6/7 = v3 (row-halo 3x3, 64-byte rows, 4 waves) 128x64 / 128x128, 10/11 = v3 (128-byte rows,
-// 8 waves) 256x64 / 128x128, 8 = v2 single-stage 1x1 (K = one tile) 128x64.
+// 8 waves) 256x64 / 128x128, 8 = v2 single-stage 1x1 (K = one tile) 128x64, 12 = v4 (3x3
+// interleaved-row tiles) 256x64, 13 = v2 7x7 row-tap layout (bf16, Cin = 8), 14 = v4 256x16
+// (narrow Cout), 15 / 16 / 17 = v2 1x1 128x256 (GEGLU) / 256x256 / 128x128 2-stage.
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -29,6 +36,18 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   const int VEh = 16 / elem_bytes;
   const bool epi_min = (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cout % VEh == 0 && a.ldy % VEh == 0 &&
                        (!a.res1 || a.ldr1 % VEh == 0) && (!a.res2 || a.ldr2 % VEh == 0);
+  if (kh == 7 && elem_bytes == 2 && a.Cin == 8 && a.K == 7 * 8 * 8 && a.zero && a.amode == 0 && !batched &&
+      !a.x2)
+    return 13;
+  if (kh == 3 && a.Cout <= 16 && a.zero && a.amode == 0 && !batched && g_conv3_force < 0 &&
+      (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / elem_bytes) == 0 && conv3_rw_host(a, 256) > 0 &&
+      conv3_rw_host(a, 256) % 64 == 0)
+    return 14;
+  if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0 && g_conv3_force < 0) {
+    const int RW = conv3_rw_host(a, 256);
+    if (RW % 64 == 0 && (a.C1 >= a.Cin || a.C1 % (64 / elem_bytes) == 0) && a.Cin % (64 / elem_bytes) == 0)
+      return 12;
+  }
   if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0) {
     if (a.Cout <= 64) return conv3_rw_host(a, 128) > 0 ? 6 : 10;
     if (conv3_rw_host(a, 128) > 0)
@@ -37,6 +56,14 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   if (v2ok) {
     if (kh == 1 && a.K <= BKE) return 8;
     if (a.Cout <= 64) return 3;
+    if (kh == 1) {
+      if (a.act == ACT_GEGLU) return 15;
+      const bool minimal = a.Cout % VEh == 0 && a.ldy % VEh == 0 && (!a.res1 || a.ldr1 % VEh == 0) &&
+                           (!a.res2 || a.ldr2 % VEh == 0) && (a.act == ACT_NONE || a.act == ACT_SILU) &&
+                           (batched || (a.Ho * a.Wo) % 256 == 0);
+      if (a.Cout >= 1024 && minimal) return 16;
+      return 17;
+    }
     if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) return 4;
     return 5;
   }

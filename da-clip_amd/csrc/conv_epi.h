@@ -71,12 +71,18 @@ DEV EpiTerms<TN> epi_terms(const ConvArgs& a, int n0, int bimg, int colbase) {
   return e;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPR, int EPK = EPI_ALL, class RowMap>
+// ILV > 1: accumulator tile i, row m of a wave holds wave pixel m * ILV + i (the interleaved
+// row order of conv3i_kernel); ILV = 1 is the plain order i * 16 + m.
+template <typename T, int BM, int BN, int WGM, int WGN, int EPR, int EPK = EPI_ALL, int ILV = 1,
+          class RowMap>
 DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
                            char* smem, int M, const RowMap& rowmap, int n0, int HWo, int bimg,
                            const EpiTerms<BN / WGN / 16>* pre = nullptr) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN, TM = WTM / 16, TN = WTN / 16;
   static_assert(EPR % WTM == 0 && BM % EPR == 0, "epilogue pass height");
+  static_assert(ILV == 1 || ILV == TM, "interleave = tiles per wave");
+  // Wave-relative row of accumulator element (tile i, lane group lg, register r).
+  auto arow = [](int i, int lg, int r) { return ILV == 1 ? i * 16 + lg * 4 + r : (lg * 4 + r) * ILV + i; };
   constexpr int NT = 64 * WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int LDW = EpiLds<BM, BN>::LDW;
@@ -84,7 +90,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
   const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
   const bool geglu = (EPK & EPI_GEGLU) && a.act == ACT_GEGLU;
-  const bool fast = !(EPK & EPI_GENERAL) || (!geglu && bimg >= 0);
+  const bool fast = !(EPK & EPI_GENERAL) || bimg >= 0;
   float* tile = reinterpret_cast<float*>(smem);
 
   T* y = reinterpret_cast<T*>(a.y);
@@ -189,16 +195,29 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
   // Phase 1a, once: bias -> scale/shift -> activation (GEGLU: x * gelu(gate) into the even
   // tile) in place on the accumulators. Doing it before the pass loop keeps the (speculated)
   // math out of the per-pass guarded stores.
-  if (fast) {
+  if (fast && geglu) {
+    // GEGLU (no scale/shift): x tile j, gate tile j+1, biases from the preloaded terms.
+    if constexpr (TN % 2 == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; j += 2)
+            acc[i][j][r] = (acc[i][j][r] + bi[j]) * gelu_fast(acc[i][j + 1][r] + bi[j + 1]);
+    }
+  } else if (fast) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          float v = (acc[i][j][r] + bi[j]) * sc[j] + sh[j];
+          // Explicit fma (and in the general path below): both paths round identically, so a
+          // row's result does not depend on whether its tile spans images (batch invariance).
+          float v = fmaf(acc[i][j][r] + bi[j], sc[j], sh[j]);
           if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_f(v);
+          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
           acc[i][j][r] = v;
         }
   } else if constexpr ((EPK & EPI_GENERAL) != 0) {
@@ -206,7 +225,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int t = wm * WTM + i * 16 + lg * 4 + r;
+        const int t = wm * WTM + arow(i, lg, r);
         if (geglu) {
           if constexpr (TN % 2 == 0) {
 #pragma unroll
@@ -214,7 +233,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
               const int nx = n0 + wn * WTN + j * 16 + lr;
               float vx = acc[i][j][r], vg = acc[i][j + 1][r];
               if (a.bias && nx < a.Cout) { vx += a.bias[nx]; vg += a.bias[nx + 16]; }
-              acc[i][j][r] = vx * gelu_f(vg);
+              acc[i][j][r] = vx * gelu_fast(vg);
             }
           }
           continue;
@@ -228,10 +247,10 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
           float v = acc[i][j][r];
           if (n < a.Cout) {
             if (a.bias) v += a.bias[n];
-            if (s) v = v * (s[n] + 1.f) + s[a.Cout + n];
+            if (s) v = fmaf(v, s[n] + 1.f, s[a.Cout + n]);
           }
           if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_f(v);
+          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
           acc[i][j][r] = v;
         }
       }
@@ -247,7 +266,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float* row = tile + (wm * WTM - r0 + i * 16 + lg * 4 + r) * LDW;
+          float* row = tile + (wm * WTM - r0 + arow(i, lg, r)) * LDW;
           if (geglu) {
             if constexpr (TN % 2 == 0) {
 #pragma unroll

@@ -13,6 +13,7 @@
 // XOR-swizzled by (row>>1)&7 so the 16 rows read by a ds_read_b128 lane group hit distinct
 // banks.
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 #include "conv_epi.h"
@@ -260,6 +261,29 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     char* st = smem + (kt % STAGES) * STAGE;
     const int k0 = kt * BKE;
     const bool kv = k0 < a.K;
+    if constexpr (KH == 7 && sizeof(T) == 2) {
+      // Row-tap layout (kernel row padded to 8 taps, Cin = 8 = one 16-byte vector): K tile kt
+      // is kernel row kh = kt, and logical slot s of a pixel row is tap kw = s (s = 7: zero).
+#pragma unroll
+      for (int j = 0; j < AG; ++j) {
+        const int kw = a_ls[j];
+        const int ih = a_ih[j] + kt, iw = a_iw[j] + kw;
+        const char* src = zero;
+        if (kv && kw < KW && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
+          src = reinterpret_cast<const char*>(x1 + (size_t)(a_pix[j] + ih * a.Ws + iw) * a.ld1);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < BG; ++j) {
+        const char* src = zero;
+        if (kv && b_row[j]) src = reinterpret_cast<const char*>(b_row[j] + k0 + b_ls[j] * VE);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + BM * 128 + (wave * BG + j) * 8 * 128),
+                                         16, 0, 0);
+      }
+      return;
+    }
     const int kpos = k0 / a.Cin;                 // wave-uniform (Cin % BKE == 0)
     const int ci0 = k0 - kpos * a.Cin;
     const int kh = kpos / KW, kw = kpos - (kpos / KW) * KW;
@@ -531,6 +555,290 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPI_MIN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
 }
 
+// ---------------------------------------------------------------------------------------
+// v4 (3x3, stride 1, pad 1): row-halo tiles with INTERLEAVED accumulator rows. A wave owns
+// WTM = 16*TM consecutive output pixels of one image row; its accumulator tile i, row m is
+// pixel m*TM + i. The kw tap of tile i then reads the same LDS rows as the kw=0 fragment of
+// tile i+kw, so one K step needs only TM+2 distinct A fragments (F_s, lane m: halo pixel
+// m*TM + s) instead of 3*TM: tile i, tap kw multiplies F_{i+kw}. That cuts the A share of the
+// LDS reads by ~2x, which (with the 64x64 wave tiles) keeps the CU's 256 B/clk LDS port below
+// the MFMA rate.
+// LDS image of a stage: the halo rows (logical row R = oy*(RW+2) + ox) then the 3*BN weight
+// rows. Bank mapping (ds_read_b128 lane groups {0-3,12-15,20-27}, ...): a fragment read
+// touches rows R0 + TM*m, so A rows are permuted within aligned groups of 4 (CK=64) or 2
+// (CK=128) rows, P(R) = (R & ~QM) | ((R + (R >> QS)) & QM), and their 16-byte slots XORed with
+// (R >> FS). The (QS, FS) pairs were found by exhaustive search over every row offset to make
+// each lane group hit 16 distinct 16-byte bank quads; weight rows are read contiguously and
+// use the TM = 1 pair. LDS-DMA writes stay lane-linear: each lane inverts P to find the
+// logical row it fills. ST-deep ring, counted vmcnt (conservative for waves with one extra
+// A instruction), one barrier per stage.
+template <int SLOTS, int TM> struct Swz;
+template <> struct Swz<4, 1> { static constexpr int QS = 0, FS = 1; };
+template <> struct Swz<4, 2> { static constexpr int QS = 2, FS = 0; };
+template <> struct Swz<4, 4> { static constexpr int QS = 2, FS = 3; };
+template <> struct Swz<4, 8> { static constexpr int QS = 3, FS = 4; };
+template <> struct Swz<8, 1> { static constexpr int QS = 0, FS = 0; };
+template <> struct Swz<8, 2> { static constexpr int QS = 1, FS = 1; };
+template <> struct Swz<8, 4> { static constexpr int QS = 2, FS = 2; };
+template <> struct Swz<8, 8> { static constexpr int QS = 3, FS = 3; };
+
+template <int SLOTS, int TM> struct RowSwz {
+  static constexpr int QM = SLOTS == 4 ? 3 : 1;
+  static constexpr int QS = Swz<SLOTS, TM>::QS, FS = Swz<SLOTS, TM>::FS;
+  static_assert(QS == 0 || (1 << QS) > QM, "P must keep the bits above QM");
+  DEV static int phys(int R) { return QS == 0 ? R : (R & ~QM) | ((R + (R >> QS)) & QM); }
+  DEV static int logical(int P) { return QS == 0 ? P : (P & ~QM) | ((P - (P >> QS)) & QM); }
+  DEV static int slot(int R, int L) { return L ^ ((R >> FS) & (SLOTS - 1)); }
+};
+
+// FL bit 0: sched_barrier fences around each stage (MFMAs stay inside their stage, so the
+// stage's DMA wait overlaps them instead of preceding them); bit 1: all B fragments of a stage
+// are read up front.
+template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN>
+__global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv3i_kernel(ConvArgs a, int RW) {
+  constexpr int NW = WGM * WGN;
+  constexpr int VE = TypeInfo<T>::VE;
+  constexpr int ES = sizeof(T);
+  constexpr int BKE = CK / ES;
+  constexpr int SLOTS = CK / 16, RPI = 64 / SLOTS;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int NF = TM + 2;                                 // distinct A fragments per K step
+  constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
+  constexpr int QM = SLOTS == 4 ? 3 : 1;
+  // Halo rows: RH*(RW+2) <= BM + 2*BM/WTM (RW >= WTM), rounded to the permutation group.
+  constexpr int NPIX_MAX = BM + 2 * (BM / WTM);
+  constexpr int NA_MAX = ((NPIX_MAX + QM) / (QM + 1) * (QM + 1) + RPI - 1) / RPI;
+  constexpr int NA_MIN = (BM + 2 + RPI - 1) / RPI;
+  constexpr int AGX = (NA_MAX + NW - 1) / NW;                // A DMA instructions per wave (max)
+  constexpr int AGN = NA_MIN / NW;                           // ... (min, for the vmcnt count)
+  constexpr int AROWS = NA_MAX * RPI;
+  constexpr int NB = 3 * BN / RPI;                           // B DMA instructions per stage
+  constexpr int BGX = (NB + NW - 1) / NW, BGN = NB / NW;     // per wave (max / min)
+  constexpr int STAGE = (AROWS + 3 * BN) * CK;
+  static_assert(SLOTS == 8 || SLOTS == 4, "CK");
+  static_assert((3 * BN) % RPI == 0 && KSTEPS >= 1 && TM >= 1 && TN >= 1, "tile");
+  static_assert(STAGE % 256 == 0 && (AROWS * CK) % 256 == 0, "bank-line aligned regions");
+  static_assert(ST == 2 || ST == 3 || ST == 4, "stages");
+  constexpr int VMW = (ST - 2) * (AGN + BGN);
+  static_assert(VMW < 64, "vmcnt");
+  // Whole-tile epilogue (one pass, residual prefetch) whenever its fp32 tile still leaves room
+  // for two blocks per CU; otherwise passes that fit in the pipeline's LDS.
+  constexpr int EPR = EpiLds<BM, BN>::BYTES <= 80 * 1024 ? BM : epi_rows<BM, BN, WTM>(ST * STAGE);
+  constexpr int SMEM = ST * STAGE > EpiLds<EPR, BN>::BYTES ? ST * STAGE : EpiLds<EPR, BN>::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  using SA = RowSwz<SLOTS, TM>;
+  using SB = RowSwz<SLOTS, 1>;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform in an SGPR
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int HWo = a.Ho * a.Wo;
+  const int rws = __builtin_ctz(RW);                      // RW is a power of two, RW % WTM == 0
+  const int RH = BM >> rws, RWP = RW + 2, NPIX = RH * RWP;
+  const int NA = ((NPIX + QM) / (QM + 1) * (QM + 1) + RPI - 1) / RPI;
+  const TileId tl = xcd_tile();
+  const int tiles_w = a.Wo >> rws;
+  const int tiles_img = (a.Ho / RH) * tiles_w;
+  const int b = tl.bx / tiles_img;
+  const int tr = tl.bx - b * tiles_img;
+  const int oh0 = (tr / tiles_w) * RH, ow0 = (tr % tiles_w) << rws;
+  const int n0 = tl.by * BN;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+  const int pixb = b * a.Hs * a.Ws;
+
+  // A DMA: instruction j of this wave fills physical rows (wave + j*NW)*RPI + lane/SLOTS.
+  int a_pix[AGX][3], a_ls[AGX];
+#pragma unroll
+  for (int j = 0; j < AGX; ++j) {
+    const int P = (wave + j * NW) * RPI + lane / SLOTS;
+    const int R = SA::logical(P);
+    a_ls[j] = SA::slot(R, lane % SLOTS) * VE;
+    const int oy = R / RWP, iw = ow0 + (R - oy * RWP) - 1;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh0 + oy + kh - 1;
+      int pix = -1;
+      if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
+        pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
+      a_pix[j][kh] = pix;
+    }
+  }
+  // B DMA: instruction j of this wave fills weight rows (wave + j*NW)*RPI + lane/SLOTS
+  // (row = tap kw * BN + channel).
+  const T* b_ptr[BGX];
+  int b_ls[BGX];
+#pragma unroll
+  for (int j = 0; j < BGX; ++j) {
+    const int row = (wave + j * NW) * RPI + lane / SLOTS;
+    b_ls[j] = SB::slot(row, lane % SLOTS) * VE;
+    const int n = n0 + row % BN;
+    b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
+                          : nullptr;
+  }
+  // Fragment offsets (stage-relative bytes).
+  const int lr = lane & 15, lg = lane >> 4;
+  int aoff[NF][KSTEPS], boff[3][TN][KSTEPS];
+  {
+    const int t0 = wm * WTM;
+    const int R0 = (t0 >> rws) * RWP + (t0 & (RW - 1)) + TM * lr;
+#pragma unroll
+    for (int s = 0; s < NF; ++s)
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks)
+        aoff[s][ks] = SA::phys(R0 + s) * CK + (SA::slot(R0 + s, ks * 4 + lg) << 4);
+  }
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int jn = 0; jn < TN; ++jn)
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const int row = kw * BN + wn * WTN + jn * 16 + lr;
+        boff[kw][jn][ks] = AROWS * CK + row * CK + (SB::slot(row, ks * 4 + lg) << 4);
+      }
+
+  // kh must be a compile-time index into a_pix (a dynamic index sends the table to scratch).
+  auto issue = [&](int c, auto khc, int buf) {
+    constexpr int kh = decltype(khc)::value;
+    char* st = smem + buf * STAGE;
+    const int ci0 = c * BKE;
+    const bool from1 = ci0 < a.C1;
+    const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) +
+                     (size_t)(from1 ? ci0 : ci0 - a.C1) * ES;
+    const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * ES;
+#pragma unroll
+    for (int j = 0; j < AGX; ++j) {
+      if (wave + j * NW < NA) {                                  // wave-uniform
+        const int pix = a_pix[j][kh];
+        const char* src = pix >= 0 ? xs + (size_t)pix * ldb + a_ls[j] * ES : zero;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + (wave + j * NW) * RPI * CK), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BGX; ++j) {
+      if (BGX == BGN || wave + j * NW < NB) {                   // wave-uniform
+        const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + kh * 3 * a.Cin + ci0 + b_ls[j])
+                                   : zero;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + AROWS * CK + (wave + j * NW) * RPI * CK),
+                                         16, 0, 0);
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const EpiTerms<TN> et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
+
+  auto compute = [&](int buf) {
+    const char* st = smem + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      u32x4 fa[NF];
+#pragma unroll
+      for (int s = 0; s < NF; ++s) fa[s] = *reinterpret_cast<const u32x4*>(st + aoff[s][ks]);
+      if constexpr (FL & 2) {
+        u32x4 fb[3][TN];
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int jn = 0; jn < TN; ++jn) fb[kw][jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[kw][jn]);
+        continue;
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        u32x4 fb[TN];
+#pragma unroll
+        for (int jn = 0; jn < TN; ++jn) fb[jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[jn]);
+      }
+    }
+  };
+
+  // Stage s = 3*c + kh. The loop is unrolled over kh so every issue() has a static kh: the
+  // stage issued at (c, kh) is s + ST - 1 = (c + (kh + ST - 1) / 3, (kh + ST - 1) % 3).
+  const int nchunk = a.Cin / BKE, S = 3 * nchunk;
+  issue(0, std::integral_constant<int, 0>{}, 0);
+  if constexpr (ST >= 3) issue(0, std::integral_constant<int, 1>{}, 1);
+  if constexpr (ST >= 4) issue(0, std::integral_constant<int, 2>{}, 2);
+  int buf = 0, nbuf = ST - 1;
+  auto step = [&](int c, auto khc) {
+    constexpr int kh = decltype(khc)::value;
+    constexpr int KN = (kh + ST - 1) % 3, CN = (kh + ST - 1) / 3;
+    const int s = 3 * c + kh;
+    if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
+    if (s + ST - 2 < S) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VMW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + ST - 1 < S) issue(c + CN, std::integral_constant<int, KN>{}, nbuf);
+    if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
+    compute(buf);
+    buf = buf + 1 == ST ? 0 : buf + 1;
+    nbuf = nbuf + 1 == ST ? 0 : nbuf + 1;
+  };
+  for (int c = 0; c < nchunk; ++c) {
+    step(c, std::integral_constant<int, 0>{});
+    step(c, std::integral_constant<int, 1>{});
+    step(c, std::integral_constant<int, 2>{});
+  }
+  struct Rows {
+    int base, rws, Wo;
+    DEV int operator()(int t) const { return base + (t >> rws) * Wo + (t & ((1 << rws) - 1)); }
+  };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK, TM>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
+}
+
+// Conv3 kernel choice override for microbenchmarks (tools/convbench): -1 = built-in choice,
+// 0 = v3 only, k > 0 = v4 configuration k of conv3i_launch.
+extern int g_conv3_force;
+extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
+
+template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN>
+bool conv3i_try(const ConvArgs& a, hipStream_t st) {
+  constexpr int WTM = BM / WGM, BKE = CK / sizeof(T);
+  const int RW = conv3_rw(a, BM);
+  if (RW <= 0 || RW % WTM || a.Cin % BKE || (a.C1 < a.Cin && a.C1 % BKE)) return false;
+  dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
+  conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
+  return true;
+}
+template <typename T>
+bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
+  switch (cfg) {
+    case 2: return conv3i_try<T, 256, 64, 4, 1, 64, 2>(a, st);
+    case 4: return conv3i_try<T, 128, 128, 2, 2, 64, 2>(a, st);
+    case 11: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 1>(a, st);
+    case 12: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 2>(a, st);
+    case 13: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 3>(a, st);
+    case 14: return conv3i_try<T, 256, 128, 4, 2, 64, 2, 1>(a, st);
+    case 15: return conv3i_try<T, 256, 128, 4, 2, 64, 2, 3>(a, st);
+    case 16: return conv3i_try<T, 256, 64, 4, 1, 64, 3, 1>(a, st);
+    case 8: return conv3i_try<T, 128, 128, 4, 2, 64, 3, 3>(a, st);
+    case 9: return conv3i_try<T, 128, 128, 4, 2, 64, 2, 3>(a, st);
+    case 10: return conv3i_try<T, 128, 64, 4, 1, 64, 2, 3>(a, st);
+    default: return false;
+  }
+}
+
 template <typename T, int KH, int KW, int S, int P>
 void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
@@ -543,12 +851,35 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   constexpr bool V2 = (KH == 1 || KH == 3 || KH == 4);
   const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
+    // Narrow output (the final conv, Cout = 3): v4 row-halo tiles with 16 output channels and
+    // the general (scalar-capable) epilogue; the A operand dominates, and v4 reads each input
+    // pixel once per kernel row instead of 9 times.
+    if (a.Cout <= 16 && a.zero && a.amode == 0 && a.w_bstride == 0 && g_conv3_force < 0 &&
+        (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / (int)sizeof(T)) == 0)
+      if (conv3i_try<T, 256, 16, 4, 1, 64, 2, 3, EPI_ALL>(a, st)) return;
+  }
+  if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
+    if (a.Cin == 8 && a.K == 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {
+      const int Mg = a.B * a.Ho * a.Wo;
+      dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, 1);
+      conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P, EPI_ALL><<<g, 512, 0, st>>>(a);
+      return;
+    }
+  }
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     const int RW = conv3_rw(a);
     // v3's epilogue is compiled for the fast case only: SiLU / none, 16-byte rows.
     const bool epi_min = (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cout % (16 / (int)sizeof(T)) == 0 &&
                          a.ldy % (16 / (int)sizeof(T)) == 0 && (!a.res1 || a.ldr1 % (16 / (int)sizeof(T)) == 0) &&
                          (!a.res2 || a.ldr2 % (16 / (int)sizeof(T)) == 0);
     if (v2ok && RW > 0 && a.w_bstride == 0 && epi_min) {
+      if (g_conv3_force > 0) {
+        if (conv3i_launch<T>(g_conv3_force, a, st)) return;
+      } else if (g_conv3_force < 0) {
+        // v4: 256 x 64 tiles, 4 waves of 64x64, interleaved rows (measured 3-15 % faster than
+        // v3 at every 3x3 shape of the UNet whose row width is a multiple of 64).
+        if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 3>(a, st)) return;
+      }
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
       // blocks share a CU and one block's LDS-DMA latency hides behind another's MFMAs
       // (measured 10-24 % faster than one 8-wave block with 128-byte rows). Small grids
@@ -591,6 +922,21 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         conv2_kernel<T, BM_, BN_, WGM_, WGN_, ST_, KH, KW, S, P, EPI_ALL><<<g, THR_, 0, st>>>(a); \
       return;                                                                                    \
     }
+    if constexpr (KH == 1) if (g_conv2_force > 0) {
+      switch (g_conv2_force) {
+        case 1: DAC_V2(256, 128, 4, 2, 3, 512)
+        case 2: DAC_V2(128, 128, 2, 2, 2, 256)
+        case 3: DAC_V2(256, 128, 4, 2, 2, 512)
+        case 4: DAC_V2(128, 128, 2, 2, 3, 256)
+        case 5: {
+          dim3 g((Mg + 255) / 256, (a.Cout + 255) / 256, gz);
+          conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_MIN><<<g, 512, 0, st>>>(a);
+          return;
+        }
+        case 6: DAC_V2(128, 256, 2, 4, 2, 512)
+        default: break;
+      }
+    }
     if constexpr (KH == 1) if (a.K <= BKE) {
       // One K tile (1x1 over 64 bf16 channels): no pipeline to fill, so a single small
       // stage (128x64, 4 waves) keeps several blocks resident per CU and their load
@@ -598,6 +944,19 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       DAC_V2(128, 64, 2, 2, 1, 256)
     }
     if (a.Cout <= 64) DAC_V2(256, 64, 4, 2, 3, 512)
+    if constexpr (KH == 1) {
+      // 1x1 / linear GEMMs with Cout > 64 (measured, tools/convbench 1x1 sweep): GEGLU projections
+      // 128x256 (8 waves of 64x64, 2 stages); wide plain outputs 256x256 (8 waves of 64x128,
+      // 2 stages, minimal epilogue only: the general one spills at this tile); the rest
+      // 128x128 with 2 stages, which keeps two blocks per CU.
+      if (a.act == ACT_GEGLU) DAC_V2(128, 256, 2, 4, 2, 512)
+      if (a.Cout >= 1024 && minimal(256)) {
+        dim3 g((Mg + 255) / 256, (a.Cout + 255) / 256, gz);
+        conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_MIN><<<g, 512, 0, st>>>(a);
+        return;
+      }
+      DAC_V2(128, 128, 2, 2, 2, 256)
+    }
     if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) DAC_V2(256, 128, 4, 2, 3, 512)
     DAC_V2(128, 128, 2, 2, 3, 256)
 #undef DAC_V2

@@ -82,19 +82,23 @@ struct Packer {
   }
   static int pad_to(int c, int v) { return (c + v - 1) / v * v; }
   // conv weight [O][C][kh][kw] (4-D key) or linear [O][C] (2-D key, kh = kw = 1).
+  // kwp > kw: each kernel row is padded to kwp taps (zero weights), so one K tile of
+  // kwp * cin elements is one kernel row (the bf16 7x7 init conv: 8 taps x 8 channels).
   ConvW conv(const std::string& key, int O, int C, int kh, int kw, const std::string& bkey = "",
-             bool linear2d = false) {
+             bool linear2d = false, int kwp = 0) {
     ConvW cw;
     cw.cout = O; cw.cin_real = C; cw.cin = pad_to(C, VE); cw.kh = kh; cw.kw = kw;
+    cw.kwp = kwp > kw ? kwp : 0;
+    const int kws = cw.kwp ? cw.kwp : kw;
     const HostW* w = linear2d ? ws.get(key, {O, C}) : ws.get(key, {O, C, kh, kw});
     if (!bkey.empty()) cw.b = f32(bkey, {O});
     if (!w) return cw;
-    std::vector<float> p((size_t)O * kh * kw * cw.cin, 0.f);
+    std::vector<float> p((size_t)O * kh * kws * cw.cin, 0.f);
     for (int o = 0; o < O; ++o)
       for (int c = 0; c < C; ++c)
         for (int y = 0; y < kh; ++y)
           for (int x = 0; x < kw; ++x)
-            p[(((size_t)o * kh + y) * kw + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
+            p[(((size_t)o * kh + y) * kws + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
     cw.w = upload_T(p);
     return cw;
   }
@@ -152,7 +156,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   const int Hin = up ? 2 * Hs : Hs, Win = up ? 2 * Ws : Ws;
   a.Ho = (Hin + 2 * pad - cw.kh) / stride + 1;
   a.Wo = (Win + 2 * pad - cw.kw) / stride + 1;
-  a.Cout = cw.cout; a.K = cw.kh * cw.kw * cw.cin; a.w = cw.w; a.bias = cw.b;
+  a.Cout = cw.cout; a.K = cw.kh * (cw.kwp ? cw.kwp : cw.kw) * cw.cin; a.w = cw.w; a.bias = cw.b;
   a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero;
@@ -365,7 +369,10 @@ struct UNetNet {
   void load(Packer<T>& P) {
     ss_total = cc_total = n_st = 0;
     if (degra) prompt = P.f32("prompt", {1, tdim});
-    init_conv = P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7);
+    // bf16: [xt | mu] has 6 (-> 8) channels = one 16-byte vector per pixel, so a K tile of 64
+    // elements is 8 neighbouring pixels of one input row (kernel row padded to 8 taps).
+    init_conv = P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", false,
+                       sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0);
     if (half) {
       half_down = P.conv("downsample.weight", nf, nf, 4, 4, "downsample.bias");
       half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias");

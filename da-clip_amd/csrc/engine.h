@@ -59,6 +59,7 @@ struct ConvW {
   const void* w = nullptr;
   const float* b = nullptr;
   int cout = 0, cin = 0, cin_real = 0, kh = 1, kw = 1;
+  int kwp = 0;   // > kw: taps of a kernel row padded to kwp with zero weights (K = kh*kwp*cin)
 };
 
 // ----------------------------------------------------------------------------- run context
