@@ -30,10 +30,17 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int b = blockIdx.z, h = blockIdx.y;
+  // XCD-aware block order: the dispatcher deals consecutive blocks to the 8 XCDs in turn, so
+  // the query tiles of one (image, head) would load its K / V into 8 different L2s. Map each
+  // XCD to a contiguous range of (query tile fastest, head, image) instead.
+  const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xq = n / 8, xr = n % 8, xcd = id % 8;
+  const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + id / 8;
+  const int bx = t % gx, h = (t / gx) % gy, b = t / (gx * gy);
   const int ld = 3 * H * D;
   const T* base = qkv + (size_t)b * L * ld;
-  const int q = blockIdx.x * 64 + wave * 16 + lr;
+  const int q = bx * 64 + wave * 16 + lr;
 
   // Q fragments (B operand of S^T = K Q^T): column = query, k = d.
   u32x4 qf[D / KSTEP];
@@ -49,22 +56,37 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int NVEC = KT * D / VE;          // 16-byte vectors per K (or V) tile
 
-  for (int k0 = 0; k0 < L; k0 += KT) {
-    __syncthreads();
-    for (int v = tid; v < NVEC; v += 256) {
+  // K / V of the next key tile are loaded into registers while this tile computes.
+  constexpr int NPT = NVEC / 256;            // vectors per thread per tile
+  static_assert(NVEC % 256 == 0, "tile");
+  u32x4 kreg[NPT], vreg[NPT];
+  auto kv_load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int v = tid + j * 256;
       const int key = v / (D / VE), dv = (v % (D / VE)) * VE;
       const int kk = k0 + key;
-      u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+      kreg[j] = vreg[j] = u32x4{0u, 0u, 0u, 0u};
       if (kk < L) {
-        kv = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + H * D + h * D + dv);
-        vv = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + 2 * H * D + h * D + dv);
+        kreg[j] = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + H * D + h * D + dv);
+        vreg[j] = *reinterpret_cast<const u32x4*>(base + (size_t)kk * ld + 2 * H * D + h * D + dv);
       }
-      *reinterpret_cast<u32x4*>(sK + key * KROW + dv * ES) = kv;
-      const T* ve = reinterpret_cast<const T*>(&vv);
+    }
+  };
+  kv_load(0);
+  for (int k0 = 0; k0 < L; k0 += KT) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int v = tid + j * 256;
+      const int key = v / (D / VE), dv = (v % (D / VE)) * VE;
+      *reinterpret_cast<u32x4*>(sK + key * KROW + dv * ES) = kreg[j];
+      const T* ve = reinterpret_cast<const T*>(&vreg[j]);
 #pragma unroll
       for (int e = 0; e < VE; ++e) *reinterpret_cast<T*>(sV + (dv + e) * VROW + key * ES) = ve[e];
     }
     __syncthreads();
+    if (k0 + KT < L) kv_load(k0 + KT);
 
     // S^T tile: 4 m-subtiles of 16 keys x this wave's 16 queries.
     f32x4 s[4];
@@ -92,13 +114,13 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float mnew = fmaxf(mrun, tmax);
-    const float corr = expf(mrun - mnew);
+    const float corr = sizeof(T) == 2 ? __expf(mrun - mnew) : expf(mrun - mnew);
     float psum = 0.f;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = expf(s[mi][r] - mnew);
+        const float p = sizeof(T) == 2 ? __expf(s[mi][r] - mnew) : expf(s[mi][r] - mnew);
         s[mi][r] = p;
         psum += p;
       }

@@ -46,7 +46,8 @@ constexpr int epi_rows(int budget) {
 // fast case (tile inside one image, SiLU / none, 16-byte aligned rows) compiles EPI_MIN and
 // stays small: the epilogue runs once per block, and every path compiled into it costs
 // instruction-cache fetches on that one pass.
-enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15 };
+enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15,
+             EPI_LN = 16 };
 
 // Per-channel epilogue terms of this lane's accumulator columns (bias, 1 + scale, shift) for a
 // tile inside image bimg; kernels that know bimg up front load them before the main loop.
@@ -98,7 +99,7 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
   const T* r2 = reinterpret_cast<const T*>(a.res2);
   // EPI_MIN kernels (single pass, vector rows): issue this thread's residual loads first, so
   // their latency overlaps the accumulator math and LDS staging below.
-  constexpr bool PREF = EPK == EPI_MIN && EPR == BM;
+  constexpr bool PREF = EPK == EPI_MIN && EPR == BM;     // (EPI_LN kernels take their own path)
   constexpr int CPRF = BN / VE;
   constexpr int NKP = PREF ? (BM * CPRF + NT - 1) / NT : 1;
   u32x4 rv1[NKP], rv2[NKP];
@@ -281,6 +282,49 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
     __syncthreads();
     const int CPR = geglu ? BN / 2 / VE : BN / VE;   // 16-byte chunks per tile row
     const int nch = EPR * CPR;
+    if constexpr ((EPK & EPI_LN) != 0) {
+      // Row LayerNorm over the BN (= Cout) channels of each tile row: the CPR threads of a row
+      // are consecutive lanes, so mean and variance are two xor-shuffle reductions (two-pass,
+      // every lane takes part: (EPR * CPR) % NT == 0 is checked at compile time).
+      static_assert((EPR * (BN / VE)) % NT == 0 && (BN / VE) <= 64, "LN epilogue tiling");
+#pragma unroll
+      for (int k = 0; k < EPR * (BN / VE) / NT; ++k) {
+        const int c = tid + k * NT;
+        const int tl = c / CPR, cc = (c % CPR) * VE;
+        const float* src = tile + tl * LDW + cc;
+        float v[VE];
+#pragma unroll
+        for (int e = 0; e < VE; e += 4) {
+          const f32x4 q = *reinterpret_cast<const f32x4*>(src + e);
+          v[e] = q[0]; v[e + 1] = q[1]; v[e + 2] = q[2]; v[e + 3] = q[3];
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) s += v[e];
+#pragma unroll
+        for (int o = 1; o < BN / VE; o <<= 1) s += __shfl_xor(s, o, 64);
+        const float mean = s / (float)BN;
+        float q = 0.f;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) { const float d = v[e] - mean; q += d * d; }
+#pragma unroll
+        for (int o = 1; o < BN / VE; o <<= 1) q += __shfl_xor(q, o, 64);
+        const float rstd = 1.f / sqrtf(q / (float)BN + a.ln_eps);
+        const int m = rowmap(r0 + tl), n = n0 + cc;
+        if (m < M) {
+#pragma unroll
+          for (int e = 0; e < VE; ++e) v[e] = (v[e] - mean) * rstd * a.ln_g[n + e];
+          float t1[VE];
+          if (r1) {
+            load_vec<T>(r1 + (size_t)m * a.ldr1 + n, t1);
+#pragma unroll
+            for (int e = 0; e < VE; ++e) v[e] += t1[e];
+          }
+          store_vec<T>(y + (size_t)m * a.ldy + n, v);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < (EPR * (BN / VE) + NT - 1) / NT; ++k) {
       const int c = tid + k * NT;

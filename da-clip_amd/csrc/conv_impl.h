@@ -758,7 +758,8 @@ conv3i_kernel(ConvArgs a, int RW) {
             for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[kw][jn]);
         continue;
       }
-#pragma unroll
+      if constexpr (FL & 4) __builtin_amdgcn_s_setprio(1);   // MFMA phase ahead of the
+#pragma unroll                                                  // other block's DMA issue
       for (int kw = 0; kw < 3; ++kw) {
         u32x4 fb[TN];
 #pragma unroll
@@ -768,6 +769,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
           for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[jn]);
       }
+      if constexpr (FL & 4) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -832,6 +834,8 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
     case 14: return conv3i_try<T, 256, 128, 4, 2, 64, 2, 1>(a, st);
     case 15: return conv3i_try<T, 256, 128, 4, 2, 64, 2, 3>(a, st);
     case 16: return conv3i_try<T, 256, 64, 4, 1, 64, 3, 1>(a, st);
+    case 17: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 5>(a, st);
+    case 18: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st);
     case 8: return conv3i_try<T, 128, 128, 4, 2, 64, 3, 3>(a, st);
     case 9: return conv3i_try<T, 128, 128, 4, 2, 64, 2, 3>(a, st);
     case 10: return conv3i_try<T, 128, 64, 4, 1, 64, 2, 3>(a, st);
@@ -878,7 +882,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       } else if (g_conv3_force < 0) {
         // v4: 256 x 64 tiles, 4 waves of 64x64, interleaved rows (measured 3-15 % faster than
         // v3 at every 3x3 shape of the UNet whose row width is a multiple of 64).
-        if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 3>(a, st)) return;
+        if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st)) return;
       }
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
       // blocks share a CU and one block's LDS-DMA latency hides behind another's MFMAs
@@ -921,6 +925,20 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       else                                                                                       \
         conv2_kernel<T, BM_, BN_, WGM_, WGN_, ST_, KH, KW, S, P, EPI_ALL><<<g, THR_, 0, st>>>(a); \
       return;                                                                                    \
+    }
+    if constexpr (KH == 1) if (a.ln_g) {
+      // Row-LayerNorm epilogue: one N tile must cover Cout exactly.
+      if (minimal(256) && a.Cout == 64) {
+        dim3 g((Mg + 255) / 256, 1, gz);
+        conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P, EPI_LN><<<g, 512, 0, st>>>(a);
+        return;
+      }
+      if (minimal(128) && a.Cout == 128) {
+        dim3 g((Mg + 127) / 128, 1, gz);
+        conv2_kernel<T, 128, 128, 2, 2, 2, KH, KW, S, P, EPI_LN><<<g, 256, 0, st>>>(a);
+        return;
+      }
+      __builtin_trap();                          // the engine only asks for these shapes
     }
     if constexpr (KH == 1) if (g_conv2_force > 0) {
       switch (g_conv2_force) {

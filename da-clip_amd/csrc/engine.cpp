@@ -159,7 +159,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.Cout = cw.cout; a.K = cw.kh * (cw.kwp ? cw.kwp : cw.kw) * cw.cin; a.w = cw.w; a.bias = cw.b;
   a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
-  a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero;
+  a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
   const double M = (double)B * a.Ho * a.Wo;
   const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   r.flops += fl;
@@ -503,14 +503,15 @@ struct UNetNet {
       r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32;
       if (!r.dry)
         linear_attention_fused<T>(x, la.gpre, la.qkv.w, q, la.wout, weff, B, H * W, C, ws, r.st);
+      // to_out (per-image weights) with its LayerNorm and the Residual in the epilogue.
       ConvW wo;
       wo.w = weff; wo.b = la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
-      T* t = r.alloc<T>(M * C);
+      T* y = r.alloc<T>(M * C);
       Epi eo;
       eo.w_bstride = (long long)C * 128;
-      conv_call<T>(r, wo, q, 128, 128, nullptr, 0, B, H, W, 0, 1, 0, t, C, eo);
-      T* y = r.alloc<T>(M * C);
-      ln<T>(r, t, C, y, C, x, C, la.gout, nullptr, (int)M, C, 1e-5f);
+      eo.ln_g = la.gout; eo.ln_eps = 1e-5f;
+      eo.res1 = x; eo.ldr1 = C;
+      conv_call<T>(r, wo, q, 128, 128, nullptr, 0, B, H, W, 0, 1, 0, y, C, eo);
       return y;
     }
     T* xn = r.alloc<T>(M * C);
@@ -540,7 +541,9 @@ struct UNetNet {
     T* xn = r.alloc<T>(M * C);
     ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
     T* gn = r.alloc<T>(M * C);
-    float* stats = r.alloc<float>((size_t)B * 64);
+    // GroupNorm workspace: partial moments [B][32 groups][GN_CHUNKS = 32][3], then the merged
+    // (mean, rstd) [B][32][2].
+    float* stats = r.alloc<float>((size_t)B * 32 * (32 * 3 + 2));
     if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
     T* hh = r.alloc<T>(M * C);
     conv_call<T>(r, s.pin, gn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, Epi());

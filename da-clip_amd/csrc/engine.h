@@ -111,6 +111,8 @@ struct Epi {
   int act = ACT_NONE;
   int amode = 0;                 // A-loader transform (ConvArgs::amode)
   long long w_bstride = 0;       // per-image weights (ConvArgs::w_bstride)
+  const float* ln_g = nullptr;   // row LayerNorm over Cout in the epilogue (ConvArgs::ln_g)
+  float ln_eps = 1e-5f;
 };
 
 template <typename T>

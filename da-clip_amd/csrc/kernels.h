@@ -35,6 +35,11 @@ struct ConvArgs {
   // > 0: per-image weights W + b * w_bstride (grid.z = B, tiles never straddle images).
   long long w_bstride;
   const void* zero;        // >= 16 zero bytes in global memory (source of padding rows)
+  // Row LayerNorm over all Cout channels (gain only, eps ln_eps) applied after bias and before
+  // the residual adds: LinearAttention's to_out LayerNorm + Residual (module_util.py:77-86,
+  // 180-185). Requires one N tile covering Cout.
+  const float* ln_g;
+  float ln_eps;
 };
 
 template <typename T>

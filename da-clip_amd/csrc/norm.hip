@@ -52,13 +52,17 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
   for (int j = 0; j < NVL; ++j) {
     const int idx = sub + G * j;
     if (idx >= NV) continue;
-    float o[VE], r[VE];
+    float o[VE], r[VE], gv[VE], bv[VE];
     if (res) load_vec<T>(res + (size_t)row * ldr + idx * VE, r);
 #pragma unroll
+    for (int e = 0; e < VE; e += 4) {
+      load_vec<float>(g + idx * VE + e, gv + e);
+      if (b) load_vec<float>(b + idx * VE + e, bv + e);
+    }
+#pragma unroll
     for (int e = 0; e < VE; ++e) {
-      const int c = idx * VE + e;
-      float t = (v[j][e] - mean) * rstd * g[c];
-      if (b) t += b[c];
+      float t = (v[j][e] - mean) * rstd * gv[e];
+      if (b) t += bv[e];
       if (res) t += r[e];
       o[e] = t;
     }
@@ -81,56 +85,105 @@ void layernorm(const void* x, int ldx, void* y, int ldy, const void* res, int ld
                                                                  b, rows, C, eps);       \
     return;                                                                              \
   }
-  if (NV <= 2) LNL(2, 1)
-  if (NV <= 4) LNL(4, 1)
-  if (NV <= 8) LNL(8, 1)
-  if (NV <= 16) LNL(16, 1)
-  if (NV <= 32) LNL(32, 1)
-  if (NV <= 64) LNL(64, 1)
-  if (NV <= 128) LNL(64, 2)
+  // Up to 4 vectors per lane: more independent loads in flight per wave and shorter shuffle
+  // chains than one vector per lane (the 512-wide token LNs ran at ~1 TB/s that way).
+  if (NV <= 1) LNL(1, 1)
+  if (NV <= 4) LNL(1, 4)
+  if (NV <= 8) LNL(2, 4)
+  if (NV <= 16) LNL(4, 4)
+  if (NV <= 32) LNL(8, 4)
+  if (NV <= 64) LNL(16, 4)
+  if (NV <= 128) LNL(32, 4)
   if (NV <= 256) LNL(64, 4)
   LNL(64, 8)
 #undef LNL
 }
 
 // ---------------------------------------------------------------------------- GroupNorm
+// Pass 1 (gn_partial): grid (GN_CHUNKS, B). A block walks a 1/GN_CHUNKS slice of one image's
+// pixels with 16-byte vector loads (thread -> fixed channel vector, pixels strided by the
+// block), keeping (count, mean, M2) per thread: each vector's VE values are reduced two-pass
+// in registers and merged with Chan's formula, which stays exact-ish where mean^2 >> var.
+// Threads of one group are then merged in a fixed order through LDS into one partial per
+// (image, chunk, group). Pass 2 (gn_apply): every thread merges its group's GN_CHUNKS
+// partials in the same fixed order (identical results everywhere), then normalises its
+// vector. Requires (C / groups) % VE == 0.
+constexpr int GN_CHUNKS = 32;
+
+struct Moments { float n, mean, m2; };
+DEV Moments chan_merge(Moments a, Moments b) {
+  const float n = a.n + b.n;
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float d = b.mean - a.mean;
+  const float wb = b.n / n;
+  Moments r;
+  r.n = n;
+  r.mean = a.mean + d * wb;
+  r.m2 = a.m2 + b.m2 + d * d * a.n * wb;
+  return r;
+}
+
 template <typename T>
-__global__ void __launch_bounds__(256) gn_stats(const T* __restrict__ x, float* stats, int HW,
-                                                int C, int groups, float eps) {
-  const int b = blockIdx.y, gi = blockIdx.x;
-  const int cpg = C / groups;
-  const int n = HW * cpg;
-  const T* base = x + (size_t)b * HW * C + gi * cpg;
-  __shared__ float red[4];
-  __shared__ float s_mean;
-  float s = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int p = i / cpg, c = i - p * cpg;
-    s += to_f(base[(size_t)p * C + c]);
+__global__ void __launch_bounds__(256) gn_partial(const T* __restrict__ x, float* part, int HW,
+                                                  int C, int groups) {
+  constexpr int VE = TypeInfo<T>::VE;
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int NV = C / VE;                         // vectors per pixel (<= 256)
+  const int ppi = 256 / NV;                      // pixels per block iteration
+  const int v = threadIdx.x % NV, p0 = threadIdx.x / NV;
+  const int pbeg = (int)((long)HW * ch / GN_CHUNKS), pend = (int)((long)HW * (ch + 1) / GN_CHUNKS);
+  Moments m{0.f, 0.f, 0.f};
+  if (p0 < ppi) {
+    const T* base = x + (size_t)b * HW * C + v * VE;
+    for (int p = pbeg + p0; p < pend; p += ppi) {
+      float f[VE];
+      load_vec<T>(base + (size_t)p * C, f);
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) s += f[e];
+      const float mu = s * (1.f / VE);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) { const float d = f[e] - mu; q += d * d; }
+      m = chan_merge(m, Moments{(float)VE, mu, q});
+    }
   }
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __shared__ float sm[3][256];
+  sm[0][threadIdx.x] = m.n; sm[1][threadIdx.x] = m.mean; sm[2][threadIdx.x] = m.m2;
   __syncthreads();
-  if (threadIdx.x == 0) s_mean = (red[0] + red[1] + red[2] + red[3]) / (float)n;
-  __syncthreads();
-  const float mean = s_mean;
-  float q = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int p = i / cpg, c = i - p * cpg;
-    const float d = to_f(base[(size_t)p * C + c]) - mean;
-    q += d * d;
-  }
-  q = wave_sum(q);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float var = (red[0] + red[1] + red[2] + red[3]) / (float)n;
-    stats[(b * groups + gi) * 2 + 0] = mean;
-    stats[(b * groups + gi) * 2 + 1] = 1.f / sqrtf(var + eps);
+  const int vpg = (C / groups) / VE;             // vectors per group
+  if ((int)threadIdx.x < groups) {
+    const int g = threadIdx.x;
+    Moments r{0.f, 0.f, 0.f};
+    for (int pp = 0; pp < ppi; ++pp)
+      for (int k = 0; k < vpg; ++k) {
+        const int t = pp * NV + g * vpg + k;
+        r = chan_merge(r, Moments{sm[0][t], sm[1][t], sm[2][t]});
+      }
+    float* o = part + (((size_t)b * groups + g) * GN_CHUNKS + ch) * 3;
+    o[0] = r.n; o[1] = r.mean; o[2] = r.m2;
   }
 }
 
+// Pass 2 (gn_merge): one thread per (image, group) merges its GN_CHUNKS partials in fixed
+// order into (mean, rstd) at part_end = part + B * groups * GN_CHUNKS * 3.
+__global__ void __launch_bounds__(64) gn_merge(float* part, int groups, float eps) {
+  const int b = blockIdx.x, g = threadIdx.x;
+  if (g >= groups) return;
+  const float* pp = part + ((size_t)b * groups + g) * GN_CHUNKS * 3;
+  float v[GN_CHUNKS * 3];                        // all loads first: one memory latency
+#pragma unroll
+  for (int k = 0; k < GN_CHUNKS * 3; ++k) v[k] = pp[k];
+  Moments r{0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < GN_CHUNKS; ++k) r = chan_merge(r, Moments{v[3 * k], v[3 * k + 1], v[3 * k + 2]});
+  float* o = part + (size_t)gridDim.x * groups * GN_CHUNKS * 3 + ((size_t)b * groups + g) * 2;
+  o[0] = r.mean;
+  o[1] = 1.f / sqrtf(r.m2 / r.n + eps);
+}
+
+// Pass 3 (gn_apply): y = (x - mean) * rstd * gamma + beta, one 16-byte vector per thread.
 template <typename T>
 __global__ void __launch_bounds__(256) gn_apply(const T* __restrict__ x, T* y,
                                                 const float* stats, const float* g,
@@ -142,25 +195,85 @@ __global__ void __launch_bounds__(256) gn_apply(const T* __restrict__ x, T* y,
   const size_t e0 = i * VE;
   const int c0 = (int)(e0 % C);
   const int b = (int)(e0 / ((size_t)HW * C));
-  const int cpg = C / groups;
-  float v[VE];
+  const float* st = stats + ((size_t)b * groups + c0 / (C / groups)) * 2;   // one group per vector
+  const float mean = st[0], rstd = st[1];
+  float v[VE], gv[VE], bv[VE];
   load_vec<T>(x + e0, v);
-#pragma unroll
-  for (int e = 0; e < VE; ++e) {
-    const int c = c0 + e, gi = c / cpg;
-    const float* s = stats + (b * groups + gi) * 2;
-    v[e] = (v[e] - s[0]) * s[1] * g[c] + bta[c];
+  load_vec<float>(g + c0, gv);                   // VE floats = 1 (f32) or 2 (bf16) vectors
+  load_vec<float>(bta + c0, bv);
+  if constexpr (VE == 8) {
+    load_vec<float>(g + c0 + 4, gv + 4);
+    load_vec<float>(bta + c0 + 4, bv + 4);
   }
+#pragma unroll
+  for (int e = 0; e < VE; ++e) v[e] = (v[e] - mean) * rstd * gv[e] + bv[e];
   store_vec<T>(y + e0, v);
+}
+
+// Fallback for groups narrower than one vector (C / groups < VE): one block per (group,
+// image), element loads, two-pass moments written as a single "chunk" (the rest zero).
+template <typename T>
+__global__ void __launch_bounds__(256) gn_partial_narrow(const T* __restrict__ x, float* part,
+                                                         int HW, int C, int groups) {
+  const int b = blockIdx.y, gi = blockIdx.x;
+  const int cpg = C / groups;
+  const int n = HW * cpg;
+  const T* base = x + (size_t)b * HW * C + gi * cpg;
+  __shared__ float red[4];
+  __shared__ float s_mean;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += to_f(base[(size_t)(i / cpg) * C + i % cpg]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) s_mean = (red[0] + red[1] + red[2] + red[3]) / (float)n;
+  __syncthreads();
+  const float mean = s_mean;
+  float q = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float d = to_f(base[(size_t)(i / cpg) * C + i % cpg]) - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  float* o = part + ((size_t)b * groups + gi) * GN_CHUNKS * 3;
+  if (threadIdx.x < GN_CHUNKS * 3) o[threadIdx.x] = 0.f;
+  if (threadIdx.x == 0) { o[0] = (float)n; o[1] = mean; o[2] = red[0] + red[1] + red[2] + red[3]; }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) gn_apply_narrow(const T* __restrict__ x, T* y,
+                                                       const float* part, const float* g,
+                                                       const float* bta, int HW, int C,
+                                                       int groups, float eps, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const int b = (int)(i / ((size_t)HW * C));
+  const float* pp = part + ((size_t)b * groups + c / (C / groups)) * GN_CHUNKS * 3;
+  const float rstd = 1.f / sqrtf(pp[2] / pp[0] + eps);
+  y[i] = from_f<T>((to_f(x[i]) - pp[1]) * rstd * g[c] + bta[c]);
 }
 
 template <typename T>
 void groupnorm(const void* x, void* y, const float* g, const float* b, int B, int HW, int C,
-               int groups, float eps, float* stats, hipStream_t st) {
-  gn_stats<T><<<dim3(groups, B), 256, 0, st>>>((const T*)x, stats, HW, C, groups, eps);
+               int groups, float eps, float* part, hipStream_t st) {
+  constexpr int VE = TypeInfo<T>::VE;
+  const int NV = C / VE;
+  if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64) {
+    gn_partial_narrow<T><<<dim3(groups, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
+    const size_t n = (size_t)B * HW * C;
+    gn_apply_narrow<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>((const T*)x, (T*)y, part, g, b,
+                                                                    HW, C, groups, eps, n);
+    return;
+  }
+  gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
+  gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
   const size_t nvec = (size_t)B * HW * C / TypeInfo<T>::VE;
-  gn_apply<T><<<(unsigned)((nvec + 255) / 256), 256, 0, st>>>((const T*)x, (T*)y, stats, g, b,
-                                                              HW, C, groups, nvec);
+  gn_apply<T><<<(unsigned)((nvec + 255) / 256), 256, 0, st>>>(
+      (const T*)x, (T*)y, part + (size_t)B * groups * GN_CHUNKS * 3, g, b, HW, C, groups, nvec);
 }
 
 #define INST(T)                                                                              \
