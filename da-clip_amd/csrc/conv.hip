@@ -18,7 +18,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // 6/7 = v3 (row-halo 3x3, 64-byte rows, 4 waves) 128x64 / 128x128, 10/11 = v3 (128-byte rows,
 // 8 waves) 256x64 / 128x128, 8 = v2 single-stage 1x1 (K = one tile) 128x64, 12 = v4 (3x3
 // interleaved-row tiles) 256x64, 13 = v2 7x7 row-tap layout (bf16, Cin = 8), 14 = v4 256x16
-// (narrow Cout), 15 / 16 / 17 = v2 1x1 128x256 (GEGLU) / 256x256 / 128x128 2-stage.
+// (narrow Cout), 15 / 16 / 17 / 18 = v2 1x1 128x256 (GEGLU) / 256x256 / 64x128 / 128x64,
+// 2-stage.
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -55,6 +56,7 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   }
   if (v2ok) {
     if (kh == 1 && a.K <= BKE) return 8;
+    if (kh == 1 && a.Cout <= 64) return 18;
     if (a.Cout <= 64) return 3;
     if (kh == 1) {
       if (a.act == ACT_GEGLU) return 15;

@@ -952,6 +952,10 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
           return;
         }
         case 6: DAC_V2(128, 256, 2, 4, 2, 512)
+        case 7: DAC_V2(128, 64, 2, 2, 2, 256)
+        case 8: DAC_V2(64, 128, 2, 2, 2, 256)
+        case 9: DAC_V2(64, 64, 2, 2, 3, 256)
+        case 10: DAC_V2(128, 64, 2, 2, 3, 256)
         default: break;
       }
     }
@@ -961,19 +965,21 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       // latencies overlap (measured best of 256x128 x {1,2,3} stages, 128x128, 128x64).
       DAC_V2(128, 64, 2, 2, 1, 256)
     }
+    if constexpr (KH == 1) if (a.Cout <= 64) DAC_V2(128, 64, 2, 2, 2, 256)
     if (a.Cout <= 64) DAC_V2(256, 64, 4, 2, 3, 512)
     if constexpr (KH == 1) {
-      // 1x1 / linear GEMMs with Cout > 64 (measured, tools/convbench 1x1 sweep): GEGLU projections
-      // 128x256 (8 waves of 64x64, 2 stages); wide plain outputs 256x256 (8 waves of 64x128,
-      // 2 stages, minimal epilogue only: the general one spills at this tile); the rest
-      // 128x128 with 2 stages, which keeps two blocks per CU.
+      // 1x1 / linear GEMMs (measured, tools/convbench 1x1 sweep): Cout <= 64 (K > 64) 128x64
+      // with 2 stages (above); GEGLU projections 128x256 (8 waves of 64x64, 2 stages); wide
+      // plain outputs 256x256 (8 waves of 64x128, 2 stages, minimal epilogue only: the
+      // general one spills at this tile); the rest 64x128 with 2 stages (4 waves of 32x64),
+      // which doubles the blocks of the small 32x32-level GEMMs over 128x128.
       if (a.act == ACT_GEGLU) DAC_V2(128, 256, 2, 4, 2, 512)
       if (a.Cout >= 1024 && minimal(256)) {
         dim3 g((Mg + 255) / 256, (a.Cout + 255) / 256, gz);
         conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_MIN><<<g, 512, 0, st>>>(a);
         return;
       }
-      DAC_V2(128, 128, 2, 2, 2, 256)
+      DAC_V2(64, 128, 2, 2, 2, 256)
     }
     if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) DAC_V2(256, 128, 4, 2, 3, 512)
     DAC_V2(128, 128, 2, 2, 3, 256)
