@@ -835,6 +835,9 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
     case 15: return conv3i_try<T, 256, 128, 4, 2, 64, 2, 3>(a, st);
     case 16: return conv3i_try<T, 256, 64, 4, 1, 64, 3, 1>(a, st);
     case 17: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 5>(a, st);
+    case 19: return conv3i_try<T, 64, 128, 2, 2, 64, 2, 4>(a, st);
+    case 20: return conv3i_try<T, 128, 64, 4, 1, 64, 2, 4>(a, st);
+    case 22: return conv3i_try<T, 64, 64, 2, 1, 64, 2, 4>(a, st);
     case 18: return conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st);
     case 8: return conv3i_try<T, 128, 128, 4, 2, 64, 3, 3>(a, st);
     case 9: return conv3i_try<T, 128, 128, 4, 2, 64, 2, 3>(a, st);
@@ -883,6 +886,10 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         // v4: 256 x 64 tiles, 4 waves of 64x64, interleaved rows (measured 3-15 % faster than
         // v3 at every 3x3 shape of the UNet whose row width is a multiple of 64).
         if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st)) return;
+        // Rows of 32 (the 32x32 level), Cout <= 256: 128x64 tiles of 32-pixel wave tiles
+        // (TM = 2), 8 % faster than v3 in the UNet; the 512-wide convs stay on v3 (v4 with
+        // 128x128 tiles measured 3-4 % slower there).
+        if (a.Cout <= 256 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 4>(a, st)) return;
       }
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
       // blocks share a CU and one block's LDS-DMA latency hides behind another's MFMAs

@@ -77,6 +77,8 @@ int main(int argc, char** argv) {
     {"L1 3x3 192->128", 8, 128, 128, 192, 128, 3, 1, 1, 0, 1, 1, 0},
     {"L2 3x3 256->256", 8, 64, 64, 256, 256, 3, 1, 1, 0, 1, 1, 0},
     {"L3 3x3 512->512", 8, 32, 32, 512, 512, 3, 1, 1, 0, 1, 1, 0},
+    {"L3 3x3 768->512", 8, 32, 32, 768, 512, 3, 1, 1, 0, 1, 1, 0},
+    {"L3 3x3 256->256", 8, 32, 32, 256, 256, 3, 1, 1, 0, 1, 1, 0},
     {"L0 1x1 64->384", 8, 256, 256, 64, 384, 1, 1, 0, 0, 0, 0, 0},
     {"L0 1x1 128->64", 8, 256, 256, 128, 64, 1, 1, 0, 0, 0, 0, 0},
     {"L1 1x1 64->384", 8, 128, 128, 64, 384, 1, 1, 0, 0, 0, 0, 0},
