@@ -268,19 +268,31 @@ struct LaCfg {
   }
 };
 
+// 16 bytes of MFMA operand (8 bf16 or 4 f32) assembled element by element.
+template <typename T> struct OpPack;
+template <> struct OpPack<bf16> {
+  bf16x8 v;
+  DEV void set(int i, float f) { v[i] = (bf16)f; }
+  DEV u32x4 get() const { return __builtin_bit_cast(u32x4, v); }
+};
+template <> struct OpPack<float> {
+  f32x4 v;
+  DEV void set(int i, float f) { v[i] = f; }
+  DEV u32x4 get() const { return __builtin_bit_cast(u32x4, v); }
+};
+
 template <typename T, int C>
-__global__ void __launch_bounds__(256) la_proj_ctx(const T* __restrict__ x, const float* __restrict__ g,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 64 ? 2 : 1, 2))) la_proj_ctx(const T* __restrict__ x, const float* __restrict__ g,
                                                    const T* __restrict__ w, T* __restrict__ qo,
                                                    float* __restrict__ part, int HW, int nc, int CH,
                                                    float eps) {
   using K = LaCfg<T, C>;
-  constexpr int VE = K::VE, TP = K::TP, PT = K::PT, KS = K::KS, KSTEP = K::KSTEP, ES = K::ES;
+  constexpr int VE = K::VE, TP = K::TP, PT = K::PT, KS = K::KS, KSTEP = K::KSTEP;
   __shared__ __attribute__((aligned(16))) char smem[K::SMEM];
   char* sx = smem;                                        // [2][TP][C] swizzled
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   char* sP = smem + 2 * K::XT + h * K::PV;                // this wave's [32][TP] P, then V
-  char* sV = sP + 32 * K::ROW;
   float* sm = reinterpret_cast<float*>(smem + 2 * K::XT + 4 * K::PV) + h * 64;
   const int b = blockIdx.y, c = blockIdx.x;
   const int p0 = c * CH, p1 = min(HW, p0 + CH);
@@ -435,23 +447,31 @@ __global__ void __launch_bounds__(256) la_proj_ctx(const T* __restrict__ x, cons
       mrun[jt] = mn;
       srun[jt] *= sc[jt];
     }
-    // P = exp(k - m) and V, transposed [channel][pixel]; padding pixels are 0.
+    // P = exp(k - m) and V straight from the projection accumulators: lane (lr, lg) holds
+    // channel lr of pixels pt*16 + lg*4 + r, which is itself a valid MFMA operand layout
+    // (row = channel, k = those pixels, the same pixel -> k map for P and V), so the context
+    // MFMA needs no LDS transpose. Padding pixels are 0.
+    constexpr int PPK = KSTEP / 16;                       // pixel tiles per k-step: 2 bf16, 1 f32
+    static_assert(PT % PPK == 0, "pixel tiles per k-step");
+    u32x4 fp[2][PT / PPK], fv[2][PT / PPK];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-      for (int pt = 0; pt < PT; ++pt) {
-        float pe[4], ve[4];
+      for (int kk = 0; kk < PT / PPK; ++kk) {
+        OpPack<T> pp, vp;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = t0 + pt * 16 + lg * 4 + r < p1;
-          pe[r] = ok ? exp_t<T>(acc[pt][jt][r] - mrun[jt]) : 0.f;
-          ve[r] = ok ? acc[pt][2 + jt][r] : 0.f;
-          srun[jt] += pe[r];
-        }
-        T* pr = reinterpret_cast<T*>(sP + (jt * 16 + lr) * K::ROW) + pt * 16 + lg * 4;
-        T* vr = reinterpret_cast<T*>(sV + (jt * 16 + lr) * K::ROW) + pt * 16 + lg * 4;
+        for (int q = 0; q < PPK; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { pr[r] = from_f<T>(pe[r]); vr[r] = from_f<T>(ve[r]); }
+          for (int r = 0; r < 4; ++r) {
+            const int pt = kk * PPK + q;
+            const bool ok = t0 + pt * 16 + lg * 4 + r < p1;
+            const float pe = ok ? exp_t<T>(acc[pt][jt][r] - mrun[jt]) : 0.f;
+            srun[jt] += pe;
+            pp.set(q * 4 + r, pe);
+            vp.set(q * 4 + r, ok ? acc[pt][2 + jt][r] : 0.f);
+          }
+        fp[jt][kk] = pp.get();
+        fv[jt][kk] = vp.get();
       }
     // Broadcast the per-channel rescale factors to the ctx accumulator layout (row d).
     if (lg == 0) { sm[lr] = sc[0]; sm[16 + lr] = sc[1]; }
@@ -466,19 +486,11 @@ __global__ void __launch_bounds__(256) la_proj_ctx(const T* __restrict__ x, cons
       }
     // ---- ctx[d][e] += sum_px P[d][px] V[e][px]
 #pragma unroll
-    for (int ks = 0; ks < TP / KSTEP; ++ks) {
-      const int k0 = (ks * KSTEP + lg * (KSTEP / 4)) * ES;
-      u32x4 fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        fa[i] = *reinterpret_cast<const u32x4*>(sP + (i * 16 + lr) * K::ROW + k0);
-        fb[i] = *reinterpret_cast<const u32x4*>(sV + (i * 16 + lr) * K::ROW + k0);
-      }
+    for (int kk = 0; kk < PT / PPK; ++kk)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) Mma<T>::run(cacc[i][j], fa[i], fb[j]);
-    }
+        for (int j = 0; j < 2; ++j) Mma<T>::run(cacc[i][j], fp[i][kk], fv[j][kk]);
     wave_sync_lds();                                      // P/V reads done before next q writes
     // ---- next tile: normalise the prefetched pixels into the other buffer.
     if (more) xstore(buf ^ 1);
