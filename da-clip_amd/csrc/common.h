@@ -86,7 +86,7 @@ DEV float gelu_fast(float x) {
   // and general paths must agree bit for bit, or results depend on batch composition).
 #pragma clang fp contract(off)
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __frcp_rn(fmaf(0.3275911f, z, 1.f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));   // v_rcp_f32, 1 ulp
   const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f),
                                    -0.284496736f), 0.254829592f);
   const float q = p * __expf(-z * z);

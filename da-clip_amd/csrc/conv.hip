@@ -19,7 +19,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // 8 waves) 256x64 / 128x128, 8 = v2 single-stage 1x1 (K = one tile) 128x64, 12 = v4 (3x3
 // interleaved-row tiles) 256x64, 13 = v2 7x7 row-tap layout (bf16, Cin = 8), 14 = v4 256x16
 // (narrow Cout), 15 / 16 / 17 / 18 = v2 1x1 128x256 (GEGLU) / 256x256 / 64x128 / 128x64,
-// 2-stage, 20 = v4 with 32-pixel wave tiles 128x64.
+// 2-stage, 20 = v4 with 32-pixel wave tiles 128x64, 21 = v5 weight-stationary 3x3 (64 -> 64).
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -44,6 +44,7 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
       (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / elem_bytes) == 0 && conv3_rw_host(a, 256) > 0 &&
       conv3_rw_host(a, 256) % 64 == 0)
     return 14;
+  if (kh == 3 && elem_bytes == 2 && (g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) return 21;
   if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0 && g_conv3_force < 0) {
     const int RW = conv3_rw_host(a, 256);
     const bool kok = (a.C1 >= a.Cin || a.C1 % (64 / elem_bytes) == 0) && a.Cin % (64 / elem_bytes) == 0;

@@ -846,6 +846,212 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
   }
 }
 
+// v5: weight-stationary 3x3 conv for Cin = Cout = 64 (bf16), the ResBlock convs of the
+// 256x256 / 128x128 levels, whose K = 576 is too short for v4's per-stage weight copies to
+// amortise. The block loads all 9 taps x 64 x 64 weights (72 KB) into LDS once and then
+// never synchronises again: each of its 8 waves owns a private 2-stage ring holding only its
+// own A halo rows (66 pixels x 32 channels per (chunk, kh) stage), so a wave's LDS-DMA wait
+// overlaps the other waves' MFMAs instead of stalling the block at a barrier. Waves walk
+// 64-pixel row segments persistently (each XCD a contiguous band of rows, for L2 reuse of
+// the kh halo rows), and the next segment's first stage is in flight during the epilogue.
+// The MFMA operands are swapped (weights as A): with weight row p holding output channel
+// 16*((p>>2)&3) + 4*(p>>4) + (p&3), each lane's accumulators are 16 consecutive channels of
+// one pixel, so the epilogue runs from registers with 16-byte residual loads and stores.
+// Epilogue: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias (EPI_MIN).
+constexpr int C3W_WAVES = 8;
+constexpr int C3W_WBYTES = 18 * 64 * 64;            // (chunk, kh, kw) regions of 64 rows x 64 B
+constexpr int C3W_STAGE = 80 * 64;                  // 5 DMA instructions of 16 halo rows
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
+  constexpr int TM = 4, NF = TM + 2, VE = 8;
+  using SA = RowSwz<4, TM>;
+  using SB = RowSwz<4, 1>;
+  __shared__ __attribute__((aligned(1024))) char smem[C3W_WBYTES + NWV * 2 * C3W_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const char* zero = reinterpret_cast<const char*>(a.zero);
+
+  // Weights -> LDS, once. DMA instruction q fills region q/4 (= (c*3 + kh)*3 + kw), rows
+  // (q%4)*16 + lane/4, 16-byte physical slot lane%4.
+  for (int q = wave; q < 72; q += NWV) {
+    const int g = q >> 2, rho = (q & 3) * 16 + (lane >> 2);
+    const int c = g / 9, tap = g % 9;
+    const int n = 16 * ((rho >> 2) & 3) + 4 * (rho >> 4) + (rho & 3);
+    const int L = SB::slot(rho, lane & 3);
+    const bf16* src = reinterpret_cast<const bf16*>(a.w) + (size_t)n * a.K + tap * 64 + c * 32 + L * VE;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + q * 1024), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // Tiles of this wave: XCD band [x*ntiles/8, (x+1)*ntiles/8), strided over the band's waves.
+  const int xcd = blockIdx.x & 7, nbx = gridDim.x >> 3;
+  const int t_end = (int)((long)(xcd + 1) * ntiles / 8);
+  const int stride = nbx * NWV;
+  int t = (int)((long)xcd * ntiles / 8) + (blockIdx.x >> 3) * NWV + wave;
+  if (t >= t_end) return;
+
+  char* ring = smem + C3W_WBYTES + wave * 2 * C3W_STAGE;
+  const char* wl = smem;
+  const int segs = a.Wo >> 6;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  // Per-lane DMA geometry: instruction j fills physical halo row j*16 + lane/4.
+  int dr[5], dls[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int R = SA::logical(j * 16 + (lane >> 2));
+    dr[j] = R;
+    dls[j] = SA::slot(R, lane & 3) * VE * 2;
+  }
+  int aoff[NF], boff[4];
+#pragma unroll
+  for (int s = 0; s < NF; ++s) aoff[s] = SA::phys(TM * lr + s) * 64 + (SA::slot(TM * lr + s, lg) << 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) boff[j] = (16 * j + lr) * 64 + (SB::slot(16 * j + lr, lg) << 4);
+
+  // Stage (c, kh) of tile tt into ring buffer buf.
+  auto issue = [&](int tt, int c, int kh, int buf) {
+    const int rr = tt / segs, ow0 = (tt - rr * segs) << 6;
+    const int b = rr / a.Ho, oh = rr - b * a.Ho;
+    const int ih = oh + kh - 1;
+    const int ci0 = c * 32;
+    const bool from1 = ci0 < a.C1;
+    const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) + (size_t)(from1 ? ci0 : ci0 - a.C1) * 2;
+    const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * 2;
+    const bool row_ok = (unsigned)ih < (unsigned)Hin;
+    const int prow = b * a.Hs + (a.up ? (ih >> 1) : ih);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int iw = ow0 + dr[j] - 1;
+      const char* src = zero;
+      if (row_ok && dr[j] < 66 && (unsigned)iw < (unsigned)Win)
+        src = xs + ((size_t)prow * a.Ws + (a.up ? (iw >> 1) : iw)) * ldb + dls[j];
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(ring + buf * C3W_STAGE + j * 1024), 16, 0, 0);
+    }
+  };
+
+  const int nb = 16 * lg;
+  float bi[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
+  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
+  bf16* y = reinterpret_cast<bf16*>(a.y);
+
+  // Waves 4-7 share SIMDs with waves 0-3: start them about half a segment later, so one
+  // wave's epilogue (VALU, SiLU transcendentals) overlaps its SIMD partner's MFMA phase.
+  if (wave & 4)
+    for (int k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(8);
+  int buf = 0;
+  issue(t, 0, 0, 0);
+  while (true) {
+    const int tn = t + stride;
+    const int rr = t / segs;
+    const int b = rr / a.Ho;
+    const int m0 = rr * a.Wo + ((t - rr * segs) << 6);
+    f32x4 acc[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 rv[TM][2];
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int c = s / 3, kh = s % 3;
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if (s < 5) issue(t, (s + 1) / 3, (s + 1) % 3, buf ^ 1);
+      else if (tn < t_end) issue(tn, 0, 0, buf ^ 1);
+      const char* st = ring + buf * C3W_STAGE;
+      u32x4 fa[NF];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) fa[f] = *reinterpret_cast<const u32x4*>(st + aoff[f]);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const char* wr = wl + ((c * 3 + kh) * 3 + kw) * 4096;
+        u32x4 fw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const u32x4*>(wr + boff[j]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[j], fa[i + kw]);
+      }
+      buf ^= 1;
+    }
+    // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15 (e = 4j + r).
+    // All residual rows are requested first, so their latency overlaps the SiLU math.
+    __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
+    if (r1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + (size_t)(m0 + TM * lr + i) * a.ldr1 + nb + 8 * h);
+    }
+    float sc[16], sh[16];
+    if (a.ss) {
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
+      const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 u = s4[q], w = h4[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const size_t m = (size_t)m0 + TM * lr + i;
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
+        if (a.act == ACT_SILU) u = silu_t<bf16>(u);
+        v[e] = u;
+      }
+      float t1[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (r1) {
+          const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
+        }
+        if (r2) {
+          load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
+        }
+        if (a.bbias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
+        }
+        store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
+      }
+    }
+    if (tn >= t_end) break;
+    t = tn;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+inline int conv3w_blocks(int ntiles) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      ncu = 256;
+  }
+  int nb = (ntiles + C3W_WAVES - 1) / C3W_WAVES;
+  if (nb > ncu) nb = ncu;
+  return (nb + 7) / 8 * 8;                          // whole XCD bands
+}
+
 template <typename T, int KH, int KW, int S, int P>
 void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
@@ -864,6 +1070,14 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     if (a.Cout <= 16 && a.zero && a.amode == 0 && a.w_bstride == 0 && g_conv3_force < 0 &&
         (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / (int)sizeof(T)) == 0)
       if (conv3i_try<T, 256, 16, 4, 1, 64, 2, 3, EPI_ALL>(a, st)) return;
+  }
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && std::is_same<T, bf16>::value) {
+    if ((g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) {
+      const int ntiles = a.B * a.Ho * (a.Wo >> 6);
+      const int delay = g_conv3_force >= 30 ? (g_conv3_force - 30) * 2 : 6;   // swept: 4-10 best
+      conv3w_kernel<C3W_WAVES><<<conv3w_blocks(ntiles), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+      return;
+    }
   }
   if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
     if (a.Cin == 8 && a.K == 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {
