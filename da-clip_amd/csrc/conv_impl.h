@@ -591,6 +591,73 @@ template <int SLOTS, int TM> struct RowSwz {
   DEV static int slot(int R, int L) { return L ^ ((R >> FS) & (SLOTS - 1)); }
 };
 
+// Register epilogue of the swapped-operand bf16 tiles (weights as the MFMA A operand, weight
+// row p holding output channel 16*((p>>2)&3) + 4*(p>>4) + (p&3) of its 64-channel tile):
+// acc[i][j][r] is channel nb + 4j + r of output row pix(i), nb = tile base + 16*(lane>>4), so
+// each lane finishes 16 consecutive channels with 16-byte loads and stores, no LDS staging.
+// EPI_MIN order: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias.
+// All residual rows are requested first, so their latency overlaps the SiLU math.
+DEV int wperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
+template <int TM, class PixOf>
+DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
+                    const PixOf& pix) {
+  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
+  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
+  bf16* y = reinterpret_cast<bf16*>(a.y);
+  __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
+  u32x4 rv[TM][2];
+  if (r1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + pix(i) * a.ldr1 + nb + 8 * h);
+  }
+  float sc[16], sh[16];
+  if (a.ss) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
+    const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 u = s4[q], w = h4[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const size_t m = pix(i);
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
+      if (a.act == ACT_SILU) u = silu_t<bf16>(u);
+      v[e] = u;
+    }
+    float t1[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (r1) {
+        const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
+      }
+      if (r2) {
+        load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
+      }
+      if (a.bbias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
+      }
+      store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
+    }
+  }
+}
+
 // FL bit 0: sched_barrier fences around each stage (MFMAs stay inside their stage, so the
 // stage's DMA wait overlaps them instead of preceding them); bit 1: all B fragments of a stage
 // are read up front.
@@ -623,10 +690,13 @@ conv3i_kernel(ConvArgs a, int RW) {
   static_assert(ST == 2 || ST == 3 || ST == 4, "stages");
   constexpr int VMW = (ST - 2) * (AGN + BGN);
   static_assert(VMW < 64, "vmcnt");
+  // FL bit 3: swapped MFMA operands (weights as A) + register epilogue (epi_regs16).
+  constexpr bool SWAP = (FL & 8) != 0;
+  static_assert(!SWAP || (WGN == 1 && BN == 64 && sizeof(T) == 2 && EPK == EPI_MIN), "swapped tiles");
   // Whole-tile epilogue (one pass, residual prefetch) whenever its fp32 tile still leaves room
   // for two blocks per CU; otherwise passes that fit in the pipeline's LDS.
   constexpr int EPR = EpiLds<BM, BN>::BYTES <= 80 * 1024 ? BM : epi_rows<BM, BN, WTM>(ST * STAGE);
-  constexpr int SMEM = ST * STAGE > EpiLds<EPR, BN>::BYTES ? ST * STAGE : EpiLds<EPR, BN>::BYTES;
+  constexpr int SMEM = ((FL & 8) || ST * STAGE > EpiLds<EPR, BN>::BYTES) ? ST * STAGE : EpiLds<EPR, BN>::BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   using SA = RowSwz<SLOTS, TM>;
   using SB = RowSwz<SLOTS, 1>;
@@ -674,7 +744,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   for (int j = 0; j < BGX; ++j) {
     const int row = (wave + j * NW) * RPI + lane / SLOTS;
     b_ls[j] = SB::slot(row, lane % SLOTS) * VE;
-    const int n = n0 + row % BN;
+    const int n = n0 + (SWAP ? wperm64(row % BN) : row % BN);
     b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
                           : nullptr;
   }
@@ -735,7 +805,8 @@ conv3i_kernel(ConvArgs a, int RW) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const EpiTerms<TN> et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
+  EpiTerms<SWAP ? 1 : TN> et;
+  if constexpr (!SWAP) et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
 
   auto compute = [&](int buf) {
     const char* st = smem + buf * STAGE;
@@ -755,7 +826,10 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[kw][jn]);
+            for (int jn = 0; jn < TN; ++jn) {
+              if constexpr (SWAP) Mma<T>::run(acc[i][jn], fb[kw][jn], fa[i + kw]);
+              else Mma<T>::run(acc[i][jn], fa[i + kw], fb[kw][jn]);
+            }
         continue;
       }
       if constexpr (FL & 4) __builtin_amdgcn_s_setprio(1);   // MFMA phase ahead of the
@@ -767,7 +841,10 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i + kw], fb[jn]);
+          for (int jn = 0; jn < TN; ++jn) {
+            if constexpr (SWAP) Mma<T>::run(acc[i][jn], fb[jn], fa[i + kw]);
+            else Mma<T>::run(acc[i][jn], fa[i + kw], fb[jn]);
+          }
       }
       if constexpr (FL & 4) __builtin_amdgcn_s_setprio(0);
     }
@@ -806,7 +883,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
-  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK, TM>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
+  if constexpr (SWAP) {
+    const int nb = n0 + 16 * lg;
+    float bi[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+    epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); });
+  } else {
+    conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK, TM>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
+  }
 }
 
 // Conv3 kernel choice override for microbenchmarks (tools/convbench): -1 = built-in choice,
@@ -842,6 +927,12 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
     case 8: return conv3i_try<T, 128, 128, 4, 2, 64, 3, 3>(a, st);
     case 9: return conv3i_try<T, 128, 128, 4, 2, 64, 2, 3>(a, st);
     case 10: return conv3i_try<T, 128, 64, 4, 1, 64, 2, 3>(a, st);
+    case 40:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st);
+      return false;
+    case 41:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st);
+      return false;
     default: return false;
   }
 }
@@ -877,7 +968,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
   for (int q = wave; q < 72; q += NWV) {
     const int g = q >> 2, rho = (q & 3) * 16 + (lane >> 2);
     const int c = g / 9, tap = g % 9;
-    const int n = 16 * ((rho >> 2) & 3) + 4 * (rho >> 4) + (rho & 3);
+    const int n = wperm64(rho);
     const int L = SB::slot(rho, lane & 3);
     const bf16* src = reinterpret_cast<const bf16*>(a.w) + (size_t)n * a.K + tap * 64 + c * 32 + L * VE;
     __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + q * 1024), 16, 0, 0);
@@ -935,9 +1026,6 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
   float bi[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
-  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
-  bf16* y = reinterpret_cast<bf16*>(a.y);
 
   // Waves 4-7 share SIMDs with waves 0-3: start them about half a segment later, so one
   // wave's epilogue (VALU, SiLU transcendentals) overlaps its SIMD partner's MFMA phase.
@@ -955,7 +1043,6 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    u32x4 rv[TM][2];
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
       const int c = s / 3, kh = s % 3;
@@ -979,60 +1066,8 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
       }
       buf ^= 1;
     }
-    // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15 (e = 4j + r).
-    // All residual rows are requested first, so their latency overlaps the SiLU math.
-    __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
-    if (r1) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + (size_t)(m0 + TM * lr + i) * a.ldr1 + nb + 8 * h);
-    }
-    float sc[16], sh[16];
-    if (a.ss) {
-      const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
-      const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 u = s4[q], w = h4[q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const size_t m = (size_t)m0 + TM * lr + i;
-      float v[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
-        if (a.act == ACT_SILU) u = silu_t<bf16>(u);
-        v[e] = u;
-      }
-      float t1[8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (r1) {
-          const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
-        }
-        if (r2) {
-          load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
-        }
-        if (a.bbias) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
-        }
-        store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
-      }
-    }
+    // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15.
+    epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; });
     if (tn >= t_end) break;
     t = tn;
   }
@@ -1099,10 +1134,16 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       } else if (g_conv3_force < 0) {
         // v4: 256 x 64 tiles, 4 waves of 64x64, interleaved rows (measured 3-15 % faster than
         // v3 at every 3x3 shape of the UNet whose row width is a multiple of 64).
+        // bf16 with whole 64-channel tiles: swapped operands + register epilogue (FL bit 3),
+        // 4-9 % faster than the LDS-staged epilogue at every v4 shape of the UNet.
+        if constexpr (sizeof(T) == 2)
+          if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) return;
         if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st)) return;
         // Rows of 32 (the 32x32 level), Cout <= 256: 128x64 tiles of 32-pixel wave tiles
         // (TM = 2), 8 % faster than v3 in the UNet; the 512-wide convs stay on v3 (v4 with
         // 128x128 tiles measured 3-4 % slower there).
+        if constexpr (sizeof(T) == 2)
+          if (a.Cout <= 256 && a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st)) return;
         if (a.Cout <= 256 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 4>(a, st)) return;
       }
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3
