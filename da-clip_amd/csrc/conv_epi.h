@@ -49,7 +49,7 @@ constexpr int epi_rows(int budget) {
 // stays small: the epilogue runs once per block, and every path compiled into it costs
 // instruction-cache fetches on that one pass.
 enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15,
-             EPI_LN = 16 };
+             EPI_LN = 16, EPI_SWAP = 32 };   // EPI_SWAP: swapped operands + epi_regs16 (conv_impl.h)
 
 // Per-channel epilogue terms of this lane's accumulator columns (bias, 1 + scale, shift) for a
 // tile inside image bimg; kernels that know bimg up front load them before the main loop.

@@ -188,6 +188,73 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 }
 
 
+// Register epilogue of the swapped-operand bf16 tiles (weights as the MFMA A operand, weight
+// row p holding output channel 16*((p>>2)&3) + 4*(p>>4) + (p&3) of its 64-channel tile):
+// acc[i][j][r] is channel nb + 4j + r of output row pix(i), nb = tile base + 16*(lane>>4), so
+// each lane finishes 16 consecutive channels with 16-byte loads and stores, no LDS staging.
+// EPI_MIN order: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias.
+// All residual rows are requested first, so their latency overlaps the SiLU math.
+DEV int wperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
+template <int TM, class PixOf>
+DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
+                    const PixOf& pix) {
+  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
+  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
+  bf16* y = reinterpret_cast<bf16*>(a.y);
+  __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
+  u32x4 rv[TM][2];
+  if (r1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + pix(i) * a.ldr1 + nb + 8 * h);
+  }
+  float sc[16], sh[16];
+  if (a.ss) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
+    const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 u = s4[q], w = h4[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const size_t m = pix(i);
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
+      if (a.act == ACT_SILU) u = silu_t<bf16>(u);
+      v[e] = u;
+    }
+    float t1[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (r1) {
+        const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
+      }
+      if (r2) {
+        load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
+      }
+      if (a.bbias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
+      }
+      store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // v2: NW = WGM*WGN waves, STAGES-deep LDS ring filled by global_load_lds (LDS-DMA, 16 B per
 // lane, no register staging). Padding rows / K tail read a 16-byte zero page. The LDS image
@@ -211,6 +278,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
   constexpr int STAGE = (BM + BN) * 128;
   static_assert(AG >= 1 && BG >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
+  constexpr bool SWAP = (EPK & EPI_SWAP) != 0;
+  static_assert(!SWAP || (EPK == EPI_SWAP && TN == 4 && sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
   constexpr int SMEM = PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES;
@@ -252,7 +321,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   for (int j = 0; j < BG; ++j) {
     const int row = (wave * BG + j) * 8 + (lane >> 3);
     b_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
-    const int n = n0 + row;
+    const int n = n0 + (SWAP ? (row & ~63) + wperm64(row & 63) : row);
     b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
   }
   const int nk = (a.K + BKE - 1) / BKE;
@@ -352,13 +421,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) Mma<T>::run(acc[i][j], fa[i], fb[j]);
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (SWAP) Mma<T>::run(acc[i][j], fb[j], fa[i]);
+          else Mma<T>::run(acc[i][j], fa[i], fb[j]);
+        }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  if constexpr (SWAP) {
+    // The dispatcher guarantees whole tiles inside one image and Cout % BN == 0.
+    const int nb = n0 + wn * WTN + 16 * lg;
+    float bi[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+    epi_regs16<TM>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+  } else {
+    conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  }
 }
 
 
@@ -590,73 +671,6 @@ template <int SLOTS, int TM> struct RowSwz {
   DEV static int logical(int P) { return QS == 0 ? P : (P & ~QM) | ((P - (P >> QS)) & QM); }
   DEV static int slot(int R, int L) { return L ^ ((R >> FS) & (SLOTS - 1)); }
 };
-
-// Register epilogue of the swapped-operand bf16 tiles (weights as the MFMA A operand, weight
-// row p holding output channel 16*((p>>2)&3) + 4*(p>>4) + (p&3) of its 64-channel tile):
-// acc[i][j][r] is channel nb + 4j + r of output row pix(i), nb = tile base + 16*(lane>>4), so
-// each lane finishes 16 consecutive channels with 16-byte loads and stores, no LDS staging.
-// EPI_MIN order: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias.
-// All residual rows are requested first, so their latency overlaps the SiLU math.
-DEV int wperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
-template <int TM, class PixOf>
-DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
-                    const PixOf& pix) {
-  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
-  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
-  bf16* y = reinterpret_cast<bf16*>(a.y);
-  __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
-  u32x4 rv[TM][2];
-  if (r1) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + pix(i) * a.ldr1 + nb + 8 * h);
-  }
-  float sc[16], sh[16];
-  if (a.ss) {
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
-    const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 u = s4[q], w = h4[q];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
-    }
-  } else {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const size_t m = pix(i);
-    float v[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
-      if (a.act == ACT_SILU) u = silu_t<bf16>(u);
-      v[e] = u;
-    }
-    float t1[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (r1) {
-        const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
-      }
-      if (r2) {
-        load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
-      }
-      if (a.bbias) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
-      }
-      store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
-    }
-  }
-}
 
 // FL bit 0: sched_barrier fences around each stage (MFMAs stay inside their stage, so the
 // stage's DMA wait overlaps them instead of preceding them); bit 1: all B fragments of a stage
@@ -1241,6 +1255,14 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_MIN><<<g, 512, 0, st>>>(a);
         return;
       }
+      // bf16, whole tiles in one image, Cout a multiple of the tile: swapped operands +
+      // register epilogue (no LDS round trip).
+      if constexpr (sizeof(T) == 2)
+        if (minimal(64) && a.Cout % 128 == 0 && g_conv2_force == 0) {
+          dim3 g((Mg + 63) / 64, a.Cout / 128, gz);
+          conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP><<<g, 256, 0, st>>>(a);
+          return;
+        }
       DAC_V2(64, 128, 2, 2, 2, 256)
     }
     if ((long)((Mg + 255) / 256) * ((a.Cout + 127) / 128) * gz >= 256) DAC_V2(256, 128, 4, 2, 3, 512)
