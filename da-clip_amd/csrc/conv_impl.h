@@ -195,7 +195,10 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 // EPI_MIN order: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias.
 // All residual rows are requested first, so their latency overlaps the SiLU math.
 DEV int wperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
-template <int TM, class PixOf>
+// LN = true (to_out of LinearAttention, Cout = 64 in one wave): row LayerNorm over the 64
+// channels held by lanes lr, lr+16, lr+32, lr+48 (two xor shuffles), gain ln_g, after the bias
+// and before the residual (module_util.py:77-86, 180-185).
+template <int TM, bool LN = false, class PixOf>
 DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
                     const PixOf& pix) {
   const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
@@ -223,6 +226,11 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
     for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
   }
+  float gl[16];
+  if constexpr (LN) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) gl[e] = a.ln_g[nb + e];
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const size_t m = pix(i);
@@ -232,6 +240,22 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
       float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
       if (a.act == ACT_SILU) u = silu_t<bf16>(u);
       v[e] = u;
+    }
+    if constexpr (LN) {
+      float sm = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) sm += v[e];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      const float mean = sm * (1.f / 64.f);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) { const float d = v[e] - mean; q += d * d; }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      const float rstd = 1.f / sqrtf(q * (1.f / 64.f) + a.ln_eps);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = (v[e] - mean) * rstd * gl[e];
     }
     float t1[8];
 #pragma unroll
@@ -279,7 +303,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   constexpr int STAGE = (BM + BN) * 128;
   static_assert(AG >= 1 && BG >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
   constexpr bool SWAP = (EPK & EPI_SWAP) != 0;
-  static_assert(!SWAP || (EPK == EPI_SWAP && TN == 4 && sizeof(T) == 2), "swapped tiles");
+  constexpr bool SLN = (EPK & EPI_LN) != 0 && SWAP;
+  static_assert(!SWAP || ((EPK == EPI_SWAP || (EPK == (EPI_SWAP | EPI_LN) && WGN == 1 && BN == 64)) && TN == 4 &&
+                          sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
   constexpr int SMEM = PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES;
@@ -436,7 +462,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     float bi[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-    epi_regs16<TM>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+    epi_regs16<TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
   } else {
     conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
   }
@@ -1204,6 +1230,13 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     }
     if constexpr (KH == 1) if (a.ln_g) {
       // Row-LayerNorm epilogue: one N tile must cover Cout exactly.
+      if constexpr (sizeof(T) == 2)
+        if (minimal(256) && a.Cout == 64 && !a.ss && a.act == ACT_NONE && !a.res2 && !a.bbias) {
+          // One wave owns all 64 channels of its rows: the LN runs in registers.
+          dim3 g((Mg + 255) / 256, 1, gz);
+          conv2_kernel<T, 256, 64, 4, 1, 2, KH, KW, S, P, EPI_SWAP | EPI_LN><<<g, 256, 0, st>>>(a);
+          return;
+        }
       if (minimal(256) && a.Cout == 64) {
         dim3 g((Mg + 255) / 256, 1, gz);
         conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P, EPI_LN><<<g, 512, 0, st>>>(a);
