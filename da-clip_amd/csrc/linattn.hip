@@ -240,6 +240,9 @@ DEV float row16_sum(float v) {
 template <typename T> DEV float exp_t(float x);
 template <> DEV float exp_t<float>(float x) { return expf(x); }
 template <> DEV float exp_t<bf16>(float x) { return __expf(x); }
+// bf16 handles: v_rcp_f32 / v_rsq_f32 (1 ulp) instead of the IEEE division / sqrt sequences.
+template <typename T> DEV float rcp_t(float x) { return sizeof(T) == 2 ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
+template <typename T> DEV float rsq_t(float x) { return sizeof(T) == 2 ? __builtin_amdgcn_rsqf(x) : 1.f / sqrtf(x); }
 
 DEV void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -350,7 +353,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
       for (int i = 0; i < VE; ++i) { const float d = v[j][i] - mean; q += d * d; }
     q += __shfl_xor(q, 1, 64);
     q += __shfl_xor(q, 2, 64);
-    const float rstd = 1.f / sqrtf(q / (float)C + eps);
+    const float rstd = rsq_t<T>(q / (float)C + eps);
     char* dst = sx + buf * K::XT;
 #pragma unroll
     for (int j = 0; j < K::QV; ++j) {
@@ -411,7 +414,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
         const float m = row16_max(fmaxf(a0, a1));
         a0 = exp_t<T>(a0 - m);
         a1 = exp_t<T>(a1 - m);
-        const float inv = 1.f / row16_sum(a0 + a1);
+        const float inv = rcp_t<T>(row16_sum(a0 + a1));
         const int px = pt * 16 + lg * 4 + r;
         sq[px * 32 + lr] = from_f<T>(a0 * inv * 0.17677669529663687f);
         sq[px * 32 + 16 + lr] = from_f<T>(a1 * inv * 0.17677669529663687f);
