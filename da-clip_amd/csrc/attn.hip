@@ -1,7 +1,7 @@
 // attn.hip — self-attention kernels.
 //
 // flash_attn_d32: SpatialTransformer self-attention (attention.py:170-193: heads = C/32,
-// d_head = 32, L = (H/8)*(W/8) tokens). Flash-style, one workgroup = 64 queries of one
+// d_head = 32, L = (H/8)*(W/8) tokens). Flash-style, one workgroup = 64 (or 128) queries of one
 // (image, head), 4 waves x 16 queries, key tiles of 64 through LDS, online softmax in fp32.
 // Computed transposed: S^T = K Q^T (A = K rows from LDS, B = this wave's 16 queries held in
 // registers) and O^T = V^T P^T. Because the S^T accumulator keeps keys in registers and
@@ -16,7 +16,7 @@
 
 namespace dac {
 
-template <typename T>
+template <typename T, int QG>
 __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qkv, T* o, int L,
                                                         int H, float scale) {
   constexpr int D = 32;
@@ -40,19 +40,29 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
   const int bx = t % gx, h = (t / gx) % gy, b = t / (gx * gy);
   const int ld = 3 * H * D;
   const T* base = qkv + (size_t)b * L * ld;
-  const int q = bx * 64 + wave * 16 + lr;
+  // QG groups of 16 queries per wave: every staged K/V tile and K fragment serves all of them.
+  int qi[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) qi[g] = bx * (64 * QG) + wave * (16 * QG) + g * 16 + lr;
 
   // Q fragments (B operand of S^T = K Q^T): column = query, k = d.
-  u32x4 qf[D / KSTEP];
+  u32x4 qf[QG][D / KSTEP];
 #pragma unroll
-  for (int s = 0; s < D / KSTEP; ++s) {
-    const int d0 = s * KSTEP + lg * (KSTEP / 4);
-    qf[s] = q < L ? *reinterpret_cast<const u32x4*>(base + (size_t)q * ld + h * D + d0)
-                  : u32x4{0u, 0u, 0u, 0u};
-  }
+  for (int g = 0; g < QG; ++g)
+#pragma unroll
+    for (int s = 0; s < D / KSTEP; ++s) {
+      const int d0 = s * KSTEP + lg * (KSTEP / 4);
+      qf[g][s] = qi[g] < L ? *reinterpret_cast<const u32x4*>(base + (size_t)qi[g] * ld + h * D + d0)
+                           : u32x4{0u, 0u, 0u, 0u};
+    }
 
-  f32x4 oacc[2] = {f32x4{0, 0, 0, 0}, f32x4{0, 0, 0, 0}};
-  float mrun = -INFINITY, lrun = 0.f;
+  f32x4 oacc[QG][2];
+  float mrun[QG], lrun[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    oacc[g][0] = oacc[g][1] = f32x4{0, 0, 0, 0};
+    mrun[g] = -INFINITY; lrun[g] = 0.f;
+  }
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int NVEC = KT * D / VE;          // 16-byte vectors per K (or V) tile
 
@@ -88,94 +98,107 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
     __syncthreads();
     if (k0 + KT < L) kv_load(k0 + KT);
 
-    // S^T tile: 4 m-subtiles of 16 keys x this wave's 16 queries.
-    f32x4 s[4];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      s[mi] = f32x4{0, 0, 0, 0};
+    for (int g = 0; g < QG; ++g) {
+      // S^T tile: 4 m-subtiles of 16 keys x this wave's 16 queries.
+      f32x4 s[4];
 #pragma unroll
-      for (int ks = 0; ks < D / KSTEP; ++ks) {
-        const int d0 = ks * KSTEP + lg * (KSTEP / 4);
-        const u32x4 ka = *reinterpret_cast<const u32x4*>(sK + (mi * 16 + lr) * KROW + d0 * ES);
-        Mma<T>::run(s[mi], ka, qf[ks]);
+      for (int mi = 0; mi < 4; ++mi) {
+        s[mi] = f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < D / KSTEP; ++ks) {
+          const int d0 = ks * KSTEP + lg * (KSTEP / 4);
+          const u32x4 ka = *reinterpret_cast<const u32x4*>(sK + (mi * 16 + lr) * KROW + d0 * ES);
+          Mma<T>::run(s[mi], ka, qf[g][ks]);
+        }
       }
-    }
-    // Online softmax over keys for this lane's query column.
-    float tmax = -INFINITY;
+      // Online softmax over keys for this lane's query column.
+      float tmax = -INFINITY;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + mi * 16 + lg * 4 + r;
-        const float v = key < L ? s[mi][r] * scale : -INFINITY;
-        s[mi][r] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mnew = fmaxf(mrun, tmax);
-    const float corr = sizeof(T) == 2 ? __expf(mrun - mnew) : expf(mrun - mnew);
-    float psum = 0.f;
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + mi * 16 + lg * 4 + r;
+          const float v = key < L ? s[mi][r] * scale : -INFINITY;
+          s[mi][r] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(mrun[g], tmax);
+      const float corr = sizeof(T) == 2 ? __expf(mrun[g] - mnew) : expf(mrun[g] - mnew);
+      float psum = 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = sizeof(T) == 2 ? __expf(s[mi][r] - mnew) : expf(s[mi][r] - mnew);
-        s[mi][r] = p;
-        psum += p;
-      }
-    psum += __shfl_xor(psum, 16, 64);
-    psum += __shfl_xor(psum, 32, 64);
-    lrun = lrun * corr + psum;
-    mrun = mnew;
+        for (int r = 0; r < 4; ++r) {
+          const float p = sizeof(T) == 2 ? __expf(s[mi][r] - mnew) : expf(s[mi][r] - mnew);
+          s[mi][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 16, 64);
+      psum += __shfl_xor(psum, 32, 64);
+      lrun[g] = lrun[g] * corr + psum;
+      mrun[g] = mnew;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) oacc[i] *= corr;
+      for (int i = 0; i < 2; ++i) oacc[g][i] *= corr;
 
-    // O^T += V^T P^T over the 64 keys.
-    if constexpr (sizeof(T) == 2) {
+      // O^T += V^T P^T over the 64 keys.
+      if constexpr (sizeof(T) == 2) {
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {           // k-step = 32 keys = subtiles 2st, 2st+1
-        bf16x8 pb;
+        for (int st = 0; st < 2; ++st) {           // k-step = 32 keys = subtiles 2st, 2st+1
+          bf16x8 pb;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pb[j] = (bf16)s[2 * st][j];
-          pb[4 + j] = (bf16)s[2 * st + 1][j];
+          for (int j = 0; j < 4; ++j) {
+            pb[j] = (bf16)s[2 * st][j];
+            pb[4 + j] = (bf16)s[2 * st + 1][j];
+          }
+          const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi) {
+            const char* row = sV + (mi * 16 + lr) * VROW;
+            uint2 lo = *reinterpret_cast<const uint2*>(row + (st * 32 + lg * 4) * ES);
+            uint2 hi = *reinterpret_cast<const uint2*>(row + (st * 32 + 16 + lg * 4) * ES);
+            Mma<T>::run(oacc[g][mi], u32x4{lo.x, lo.y, hi.x, hi.y}, pbu);
+          }
         }
-        const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
+      } else {
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const char* row = sV + (mi * 16 + lr) * VROW;
-          uint2 lo = *reinterpret_cast<const uint2*>(row + (st * 32 + lg * 4) * ES);
-          uint2 hi = *reinterpret_cast<const uint2*>(row + (st * 32 + 16 + lg * 4) * ES);
-          Mma<T>::run(oacc[mi], u32x4{lo.x, lo.y, hi.x, hi.y}, pbu);
-        }
-      }
-    } else {
+        for (int st = 0; st < 4; ++st) {           // k-step = 16 keys = subtile st
+          const u32x4 pbu = __builtin_bit_cast(u32x4, s[st]);
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {           // k-step = 16 keys = subtile st
-        const u32x4 pbu = __builtin_bit_cast(u32x4, s[st]);
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi) {
-          const u32x4 va = *reinterpret_cast<const u32x4*>(sV + (mi * 16 + lr) * VROW +
-                                                           (st * 16 + lg * 4) * ES);
-          Mma<T>::run(oacc[mi], va, pbu);
+          for (int mi = 0; mi < 2; ++mi) {
+            const u32x4 va = *reinterpret_cast<const u32x4*>(sV + (mi * 16 + lr) * VROW +
+                                                             (st * 16 + lg * 4) * ES);
+            Mma<T>::run(oacc[g][mi], va, pbu);
+          }
         }
       }
     }
   }
-  if (q >= L) return;
-  const float inv = 1.f / lrun;
-  T* out = o + ((size_t)b * L + q) * (H * D) + h * D;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int g = 0; g < QG; ++g) {
+    if (qi[g] >= L) continue;
+    const float inv = 1.f / lrun[g];
+    T* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) out[mi * 16 + lg * 4 + r] = from_f<T>(oacc[mi][r] * inv);
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[mi * 16 + lg * 4 + r] = from_f<T>(oacc[g][mi][r] * inv);
+  }
 }
 
 template <typename T>
 void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
-  dim3 g((L + 63) / 64, H, B);
-  flash_d32_kernel<T><<<g, 256, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+  // Two 16-query groups per wave (128 queries per block) once that still leaves >= 2 blocks
+  // per CU: each staged K/V tile and its two barriers then serve twice the queries.
+  if ((long)((L + 127) / 128) * H * B >= 512) {
+    dim3 g((L + 127) / 128, H, B);
+    flash_d32_kernel<T, 2><<<g, 256, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+  } else {
+    dim3 g((L + 63) / 64, H, B);
+    flash_d32_kernel<T, 1><<<g, 256, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+  }
 }
 
 // ------------------------------------------------------------------------------ small MHA
