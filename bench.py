@@ -64,7 +64,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the bf16-vs-fp32 PSNR sample")
-    p.add_argument("--cpu-steps", type=int, default=2, help="UNet steps in the CPU sample")
+    p.add_argument("--cpu-steps", type=int, default=5, help="UNet steps in the CPU sample (>= 5)")
     a = p.parse_args()
     wild = a.model == "wild-ir"
     a.batch = a.batch or (2 if wild else 8)
@@ -92,14 +92,28 @@ def setup_dist(args):
     return ws, rank, local
 
 
+def host_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup v2 CPU
+    quota when one is set (a GPU box shows the whole machine in os.cpu_count())."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(args, sd_unet, sd_clip):
-    """Oracle (numpy fp32 restatement of the reference path) on the host cores: DaCLIP encode
-    of one 224^2 image + `cpu_steps` of the 100 UNet+posterior steps at 256^2, B=1; the
-    per-image time is encode + 100 x mean step time."""
+    """Oracle (numpy fp32 restatement of the reference path) on all host cores available to
+    this process: DaCLIP encode of one 224^2 image + `cpu_steps` (>= 5) of the 100
+    UNet+posterior steps at 256^2, B=1; per-image time = encode + 100 x mean step time
+    (SURVEY.md §8d allows timing T=5 and scaling linearly)."""
     from threadpoolctl import threadpool_limits
     from oracle import clip as OC, sde as OS, unet as OU
     from daclip_amd import synth
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cores = host_cores()
     with threadpool_limits(limits=cores):
         img = synth.synth_noise((1, 3, 224, 224), seed=3, tag="cpu_img")
         lq = synth.synth_images(1, args.res, args.res, seed=4)
@@ -117,15 +131,45 @@ def cpu_baseline(args, sd_unet, sd_clip):
         t_step = (time.perf_counter() - t0) / args.cpu_steps
     per_img = t_enc + args.T * t_step
     return {"value": 1.0 / per_img, "unit": "images/s", "cores": cores, "kind": "port",
+            "host_cpus_visible": os.cpu_count(),
             "sample": f"B=1 {args.res}x{args.res}: 1 DaCLIP encode ({t_enc:.2f}s) + {args.cpu_steps} "
                       f"of {args.T} UNet+posterior steps ({t_step:.2f}s each), numpy fp32 oracle; "
                       f"per-image time = encode + {args.T} x step"}
 
 
+def psnr_vs_reference(args, clip, unet, dev):
+    """PSNR parity of the benchmarked mode against the REFERENCE CPU path: the headline fixture
+    (tests/golden/headline_256_t100.npz, made by running the reference's predict.py flow on
+    images/00006.jpg with the same seeded weights and injected noise) is restored by this
+    run's own encoder + UNet handles (B=1, 256^2, T=100). delta_db = PSNR(ours, LQ) -
+    PSNR(reference, LQ) (no GT exists for the image); north-star bar |delta_db| < 1e-3."""
+    from daclip_amd import synth
+    from daclip_amd.sde import IRSDE
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    t0 = time.perf_counter()
+    g = np.load(os.path.join(ROOT, "tests", "golden", "headline_256_t100.npz"))
+    lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0).to(dev)
+    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=71, tag="hl_noise_state")).to(dev)
+    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=72, tag="hl_steps")).to(dev)
+    ic, dc = clip.encode_image(torch.from_numpy(g["img4clip"]).to(dev), control=True)
+    s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+    s.set_model(unet)
+    s.set_mu(lq)
+    out = s.reverse_posterior(s.noise_state(lq, noise=ns), noises=zs, text_context=dc, image_context=ic)
+    u8 = tensor2img(out[0])
+    ref = g["out"][0]
+    o = out[0].cpu().numpy()
+    return {"vs": "reference CPU path (tests/golden/headline_256_t100.npz: predict.py flow, images/00006.jpg, "
+                  "same seeded weights + injected noise)",
+            "delta_db": round(float(calculate_psnr(u8, g["lq_u8"]) - calculate_psnr(g["out_u8"], g["lq_u8"])), 6),
+            "psnr_vs_reference_u8_db": round(float(calculate_psnr(u8, g["out_u8"])), 3),
+            "out_max_rel_err": float(np.abs(o - ref).max() / np.abs(ref).max()),
+            "sample": f"B=1 256x256 T=100 restore in the benchmarked dtype ({time.perf_counter() - t0:.1f}s)"}
+
+
 def psnr_sample(args, wu_keys, clip, unet_bf16, lq, img, dev):
-    """PSNR of the bf16 restore vs the fp32 (parity-mode) restore of image 0 at the bench
-    resolution, same contexts, same injected noise. The fp32 path reproduces the reference's
-    uint8 output bit-exactly on the T=100 golden fixture (tests/test_hip_parity.py)."""
+    """Wild-IR (no reference fixture at 512^2): PSNR of the bf16 restore vs the fp32
+    (parity-mode) restore of image 0 at the bench resolution, same contexts and noise."""
     from daclip_amd import synth
     from daclip_amd.unet import ConditionalUNet
     from daclip_amd.sde import IRSDE
@@ -239,8 +283,11 @@ def main():
         h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
 
     psnr = None
-    if rank == 0 and not args.no_psnr and args.dtype == "bf16":
-        psnr = psnr_sample(args, wu_keys=uspec, clip=clip, unet_bf16=unet, lq=lq[:1], img=img4clip[:1], dev=dev)
+    if rank == 0 and not args.no_psnr:
+        if args.model == "universal-ir" and args.T == 100:
+            psnr = psnr_vs_reference(args, clip, unet, dev)
+        elif args.dtype == "bf16":
+            psnr = psnr_sample(args, wu_keys=uspec, clip=clip, unet_bf16=unet, lq=lq[:1], img=img4clip[:1], dev=dev)
 
     if rank == 0:
         images = n_glob * args.steps
@@ -283,7 +330,8 @@ def main():
                           "sampler": "posterior", "parallelism": f"dp{ws}"},
                "model_tflop_per_image": round(total_tf, 3),
                "whole_path_tflops": round(total_tf * images / el, 1),
-               "roofline": roof, "outputs_finite": finite, "psnr": psnr}
+               "roofline": roof, "outputs_finite": finite, "psnr": psnr,
+               "build": _lib.build_info()}
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, synth.synth_state_dict(uspec, 0),
                                                synth.synth_state_dict(cspec, 0))

@@ -73,9 +73,12 @@ int dac_create(int device, int dtype, const dac_config* cfg, dac_handle** out) {
   h->dtype = dtype;
   h->cfg = *cfg;
   int rc = guard(h, [&]() -> int {
+    // in_nc = out_nc = 3: the sampler consumes the noise prediction as an image-shaped
+    // tensor (sde_utils.py:245-247), and the output / step kernels are laid out for 3 channels.
     if (cfg->unet && (cfg->depth < 1 || cfg->depth > 8 || cfg->nf % 32 || cfg->in_nc != 3 ||
-                      cfg->out_nc > 16))
-      throw dac::Error(DAC_E_ARG, "unsupported UNet config");
+                      cfg->out_nc != 3))
+      throw dac::Error(DAC_E_ARG, "unsupported UNet config (needs in_nc = out_nc = 3, nf % 32 == 0, "
+                                  "1 <= depth <= 8)");
     h->eng = dac::make_engine(device, dtype, *cfg);
     return DAC_OK;
   });
@@ -214,6 +217,18 @@ int dac_sde_schedule(dac_handle* h, float max_sigma, int T, int schedule, float 
   });
 }
 
+int dac_sde_set_time_scale(dac_handle* h, double scale) {
+  return guard(h, [&]() -> int {
+    if (!(scale > 0.0) || !std::isfinite(scale)) throw dac::Error(DAC_E_ARG, "time scale must be > 0");
+    auto& s = h->eng->sched;
+    if (s.time_scale != scale) {
+      s.time_scale = scale;
+      h->eng->invalidate_graphs();
+    }
+    return DAC_OK;
+  });
+}
+
 int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu, const float* text_ctx,
                     const float* image_ctx, int B, int H, int W, int T, const float* noise,
                     uint64_t seed, void* stream) {
@@ -312,5 +327,10 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
 }
 
 const char* dac_last_error(dac_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+#ifndef DAC_BUILD_ID
+#define DAC_BUILD_ID "unknown"
+#endif
+const char* dac_build_id(void) { return DAC_BUILD_ID; }
 
 }  // extern "C"

@@ -278,6 +278,9 @@ struct UNetNet {
   struct ST { const float* gpre = nullptr; const float *gnw = nullptr, *gnb = nullptr;
               ConvW pin; const float *n1w = nullptr, *n1b = nullptr, *n3w = nullptr, *n3b = nullptr;
               ConvW qkv, o, ff1, ff2, pout; const float *a2v = nullptr, *a2o = nullptr, *a2ob = nullptr;
+              // attn2 without a context is self-attention over norm2(x) (attention.py:174);
+              // it needs context_dim == C, as in the reference (to_k / to_v take C inputs).
+              bool self_ok = false; ConvW qkv2, o2; const float *n2w = nullptr, *n2b = nullptr;
               int cc_off = 0; };
   struct Attn { bool st = false; LA la; ST s; };
   struct Level { RB b1, b2; Attn at; ConvW samp; };
@@ -355,8 +358,13 @@ struct UNetNet {
     s.a2ob = P.f32(b + "attn2.to_out.0.bias", {C});
     s.n1w = P.f32(b + "norm1.weight", {C});
     s.n1b = P.f32(b + "norm1.bias", {C});
-    (void)P.f32(b + "norm2.weight", {C});
-    (void)P.f32(b + "norm2.bias", {C});
+    s.n2w = P.f32(b + "norm2.weight", {C});
+    s.n2b = P.f32(b + "norm2.bias", {C});
+    if (ctx == C) {              // image_context=None falls back to self-attention
+      s.self_ok = true;
+      s.qkv2 = P.concat({b + "attn2.to_q.weight", b + "attn2.to_k.weight", b + "attn2.to_v.weight"}, C, C);
+      s.o2 = P.linear(b + "attn2.to_out.0.weight", C, C, b + "attn2.to_out.0.bias");
+    }
     s.n3w = P.f32(b + "norm3.weight", {C});
     s.n3b = P.f32(b + "norm3.bias", {C});
     s.pout = P.conv(f + "proj_out.weight", C, C, 1, 1, f + "proj_out.bias");
@@ -423,10 +431,12 @@ struct UNetNet {
   // ----------------------------------------------------------------- per-call tables
   // ss_all[(i*B + b)*ss_total + off ...]: ResBlock (scale, shift) for step i, image b, whose
   // time is t0 + dt * i. sin_tab: [nT*B][nf] device scratch for the sinusoidal embeddings.
-  void tables(Run& r, float* sin_tab, int nT, float t0, float dt, const float* tc,
+  // Step i's time is (t0 + dt * i) * scale (IRSDE.sample_scale); tc / icx may be null (no
+  // prompt embedding / no cross-attention constants, DenoisingUNet_arch.py:133-140).
+  void tables(Run& r, float* sin_tab, int nT, double t0, double dt, double scale, const float* tc,
               const float* icx, int B, float* ss_all, float* cc) {
     const int R = nT * B;
-    if (!r.dry) sinus_embedding(sin_tab, R, B, nf, t0, dt, r.st);
+    if (!r.dry) sinus_embedding(sin_tab, R, B, nf, t0, dt, scale, r.st);
     float* h1 = r.alloc<float>((size_t)R * tdim);
     float* temb = r.alloc<float>((size_t)R * tdim);
     float* pe = nullptr;
@@ -464,6 +474,7 @@ struct UNetNet {
                      ACT_NONE, nullptr, 0, 1, r.st);
       }
     };
+    if (!icx) return;
     for (auto& L : downs) stc(L.at);
     stc(mid_attn);
     for (auto& L : ups) stc(L.at);
@@ -556,8 +567,31 @@ struct UNetNet {
     if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, 0.17677669529663687f, r.st);
     T* h2 = r.alloc<T>(M * C);
     Epi e;
-    e.res1 = hh; e.ldr1 = C; e.bbias = cc + s.cc_off; e.bb_ld = cc_total;
+    e.res1 = hh; e.ldr1 = C;
+    if (cc) {
+      // attn2 over the single context token folded in as a per-image bias (see load_attn).
+      e.bbias = cc + s.cc_off; e.bb_ld = cc_total;
+    }
     conv_call<T>(r, s.o, o, C, C, nullptr, 0, B, H, W, 0, 1, 0, h2, C, e);
+    if (!cc) {
+      // No image context: attn2 is self-attention over norm2(x) (attention.py:174, 212).
+      if (!s.self_ok)
+        throw Error(DAC_E_ARG, "image_context is None: cross-attention falls back to self-attention, which "
+                               "needs context_dim == channels (the reference fails with 'mat1 and mat2 "
+                               "shapes cannot be multiplied')");
+      T* a2 = r.alloc<T>(M * C);
+      ln<T>(r, h2, C, a2, C, nullptr, 0, s.n2w, s.n2b, (int)M, C, 1e-5f);
+      T* qkv2 = r.alloc<T>(M * 3 * C);
+      conv_call<T>(r, s.qkv2, a2, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv2, 3 * C, Epi());
+      T* o2 = r.alloc<T>(M * C);
+      r.flops += 4.0 * B * (double)L * L * C;
+      if (!r.dry) flash_attn_d32<T>(qkv2, o2, B, L, C / 32, 0.17677669529663687f, r.st);
+      T* h3 = r.alloc<T>(M * C);
+      Epi e3;
+      e3.res1 = h2; e3.ldr1 = C;
+      conv_call<T>(r, s.o2, o2, C, C, nullptr, 0, B, H, W, 0, 1, 0, h3, C, e3);
+      h2 = h3;
+    }
     T* f = r.alloc<T>(M * C);
     ln<T>(r, h2, C, f, C, nullptr, 0, s.n3w, s.n3b, (int)M, C, 1e-5f);
     T* g = r.alloc<T>(M * 4 * C);
@@ -879,6 +913,7 @@ class EngineT : public Engine {
   struct Bufs {
     float *xs = nullptr, *mus = nullptr, *tcs = nullptr, *ics = nullptr, *ss = nullptr,
           *cc = nullptr, *sin = nullptr;
+    float* noise = nullptr;       // owned copy of injected noise [nT,B,3,H,W] (lazily allocated)
     void* out = nullptr;
     uint64_t* seed = nullptr;
     int ldo = 0;
@@ -886,7 +921,7 @@ class EngineT : public Engine {
   std::map<std::tuple<int, int, int, int>, Bufs> bufs;    // (B, H, W, nT)
   void free_bufs(Bufs& b) {
     for (void* p : {(void*)b.xs, (void*)b.mus, (void*)b.tcs, (void*)b.ics, (void*)b.ss,
-                    (void*)b.cc, (void*)b.sin, b.out, (void*)b.seed})
+                    (void*)b.cc, (void*)b.sin, (void*)b.noise, b.out, (void*)b.seed})
       if (p) (void)hipFree(p);
   }
   // DAC_POISON=1: fill fresh workspace with 0xFF bytes (NaN in f32/bf16) so any
@@ -902,10 +937,19 @@ class EngineT : public Engine {
     if (poison()) HIP_OK(hipMemset(p, 0xFF, bytes));
     return (X*)p;
   }
+  // Loop buffers per shape. Graphs bake these addresses in, so the shape cache is bounded
+  // by dropping every graph together with the buffers when it grows past kMaxShapes.
+  static constexpr size_t kMaxShapes = 8;
   Bufs& get_bufs(int B, int H, int W, int nT) {
     auto key = std::make_tuple(B, H, W, nT);
     auto it = bufs.find(key);
     if (it != bufs.end()) return it->second;
+    if (bufs.size() >= kMaxShapes) {
+      HIP_OK(hipDeviceSynchronize());
+      clear_graphs();
+      for (auto& kv : bufs) free_bufs(kv.second);
+      bufs.clear();
+    }
     Bufs b;
     const size_t n = (size_t)B * 3 * H * W;
     const int Hp = unet->pad_of(H), Wp = unet->pad_of(W);
@@ -921,16 +965,19 @@ class EngineT : public Engine {
     b.seed = dalloc<uint64_t>(2);     // [seed, element offset of image 0]
     return bufs.emplace(key, b).first->second;
   }
-  size_t plan_unet(int B, int H, int W, int nT) {
+  // Dry run of the same launch sequence: arena size (and argument checks, e.g. the
+  // self-attention fallback) before anything is launched or captured.
+  size_t plan_unet(int B, int H, int W, int nT, bool has_ic) {
     Arena a;
     a.dry = true;
     Run r;
     r.dry = true;
     r.ar = &a;
-    unet->tables(r, nullptr, nT, 0.f, 0.f, (const float*)1, (const float*)1, B, nullptr, nullptr);
+    const float* dummy = (const float*)1;
+    unet->tables(r, nullptr, nT, 0.0, 0.0, 1.0, dummy, has_ic ? dummy : nullptr, B, nullptr, nullptr);
     const size_t t = a.peak;
     a.reset();
-    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, nullptr, nullptr, 4);
+    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, has_ic ? dummy : nullptr, nullptr, 4);
     return std::max(t, a.peak) + (1 << 20);
   }
   Run live(hipStream_t st) {
@@ -979,15 +1026,16 @@ class EngineT : public Engine {
   void unet_forward(const float* xt, const float* mu, float t, const float* tc, const float* icx,
                     int B, int H, int W, float* eps, hipStream_t st) override {
     need(unet != nullptr, "handle has no UNet");
-    need(!(unet->n_st > 0 && icx == nullptr), "image_context is required (SpatialTransformer)");
     HIP_OK(hipSetDevice(dev));
-    ensure_arena(plan_unet(B, H, W, 1));
+    const float* tcu = unet->degra ? tc : nullptr;
+    const float* icu = unet->imgctx ? icx : nullptr;
+    ensure_arena(plan_unet(B, H, W, 1, icu != nullptr));
     Bufs& b = get_bufs(B, H, W, 1);
     Run r = live(st);
     arena.reset();
-    unet->tables(r, b.sin, 1, t, 0.f, tc, icx, B, b.ss, b.cc);
+    unet->tables(r, b.sin, 1, (double)t, 0.0, 1.0, tcu, icu, B, b.ss, b.cc);
     arena.reset();
-    unet->forward(r, xt, mu, B, H, W, b.ss, b.cc, b.out, b.ldo);
+    unet->forward(r, xt, mu, B, H, W, b.ss, icu ? b.cc : nullptr, b.out, b.ldo);
     unet_out<T>(b.out, b.ldo, eps, B, H, W, unet->pad_of(H), unet->pad_of(W), st);
     HIP_OK(hipGetLastError());
   }
@@ -1005,11 +1053,13 @@ class EngineT : public Engine {
   }
 
   // ------------------------------------------------------------------ full loop
+  // One captured loop per (mode | feature bits, shape). Feature bits: 2 = no text context
+  // (no prompt embedding), 4 = no image context (self-attention attn2), 8 = injected noise
+  // (read from the handle-owned copy, so the caller's pointer is not part of the key).
   struct GKey {
     int mode, B, H, W, nT;
-    const float* noise;
     bool operator<(const GKey& o) const {
-      return std::tie(mode, B, H, W, nT, noise) < std::tie(o.mode, o.B, o.H, o.W, o.nT, o.noise);
+      return std::tie(mode, B, H, W, nT) < std::tie(o.mode, o.B, o.H, o.W, o.nT);
     }
   };
   std::map<GKey, hipGraphExec_t> graphs;
@@ -1017,17 +1067,21 @@ class EngineT : public Engine {
     for (auto& kv : graphs) (void)hipGraphExecDestroy(kv.second);
     graphs.clear();
   }
-  void record_loop(Run& r, Bufs& b, int mode, int B, int H, int W, int nT, const float* noise) {
+  void record_loop(Run& r, Bufs& b, int mode, int B, int H, int W, int nT, bool has_noise,
+                   bool has_tc, bool has_ic) {
     const int Hp = unet->pad_of(H), Wp = unet->pad_of(W);
     r.ar->reset();
-    unet->tables(r, b.sin, nT, (float)nT, -1.f, b.tcs, b.ics, B, b.ss, b.cc);
+    // Step i runs the model at time (T - i) * sample_scale (sde_utils.py:302).
+    unet->tables(r, b.sin, nT, (double)nT, -1.0, sched.time_scale, has_tc ? b.tcs : nullptr,
+                 has_ic ? b.ics : nullptr, B, b.ss, b.cc);
     const size_t n = (size_t)B * 3 * H * W;
     for (int i = 0; i < nT; ++i) {
       const int t = nT - i;
       r.ar->reset();
-      unet->forward(r, b.xs, b.mus, B, H, W, b.ss + (size_t)i * B * unet->ss_total, b.cc, b.out, b.ldo);
+      unet->forward(r, b.xs, b.mus, B, H, W, b.ss + (size_t)i * B * unet->ss_total, has_ic ? b.cc : nullptr,
+                    b.out, b.ldo);
       if (!r.dry)
-        sde_step<T>(mode, b.xs, b.mus, b.out, b.ldo, Hp, Wp, noise ? noise + (size_t)i * n : nullptr,
+        sde_step<T>(mode, b.xs, b.mus, b.out, b.ldo, Hp, Wp, has_noise ? b.noise + (size_t)i * n : nullptr,
                     b.seed, (uint32_t)t, sched.coef(t, mode), B, H, W, r.st);
     }
   }
@@ -1036,27 +1090,28 @@ class EngineT : public Engine {
     need(unet != nullptr, "handle has no UNet");
     need(sched.T > 0, "call dac_sde_schedule first");
     need(nT >= 1 && nT <= sched.T, "T exceeds the schedule length");
-    need(!(unet->n_st > 0 && icx == nullptr), "image_context is required (SpatialTransformer)");
     HIP_OK(hipSetDevice(dev));
-    ensure_arena(plan_unet(B, H, W, nT));
+    const bool has_tc = tc != nullptr && unet->degra;
+    const bool has_ic = icx != nullptr && unet->imgctx;
+    const bool has_noise = noise != nullptr;
+    ensure_arena(plan_unet(B, H, W, nT, has_ic));
     Bufs& b = get_bufs(B, H, W, nT);
     const size_t n = (size_t)B * 3 * H * W;
+    if (has_noise && !b.noise) b.noise = dalloc<float>((size_t)nT * n);
     HIP_OK(hipEventRecord(ev_in, st));
     HIP_OK(hipStreamWaitEvent(priv, ev_in, 0));
     HIP_OK(hipMemcpyAsync(b.xs, x, n * 4, hipMemcpyDeviceToDevice, priv));
     HIP_OK(hipMemcpyAsync(b.mus, mu, n * 4, hipMemcpyDeviceToDevice, priv));
-    if (tc) HIP_OK(hipMemcpyAsync(b.tcs, tc, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
-    if (icx) HIP_OK(hipMemcpyAsync(b.ics, icx, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
-    seed_host[0] = seed;
-    seed_host[1] = noise_offset * (uint64_t)(3 * H * W);
-    HIP_OK(hipMemcpyAsync(b.seed, seed_host, 16, hipMemcpyHostToDevice, priv));
-    HIP_OK(hipStreamSynchronize(priv));       // seed_host staging is pageable
-    // tc == nullptr is a different program (no prompt embedding): key it via mode bit.
-    const int mkey = mode | (tc ? 0 : 2);
+    if (has_tc) HIP_OK(hipMemcpyAsync(b.tcs, tc, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
+    if (has_ic) HIP_OK(hipMemcpyAsync(b.ics, icx, (size_t)B * unet->ctx * 4, hipMemcpyDeviceToDevice, priv));
+    if (has_noise) HIP_OK(hipMemcpyAsync(b.noise, noise, (size_t)nT * n * 4, hipMemcpyDeviceToDevice, priv));
+    // Noise key [seed, element offset of image 0], written in stream order by a kernel.
+    set_u64x2(b.seed, seed, noise_offset * (uint64_t)(3 * H * W), priv);
+    const int mkey = mode | (has_tc ? 0 : 2) | (has_ic ? 0 : 4) | (has_noise ? 8 : 0);
     static const bool no_graph = getenv("DAC_NO_GRAPH") && getenv("DAC_NO_GRAPH")[0] == '1';
     if (no_graph && prof.kernel_id < 0) {
       Run r = live(priv);
-      record_loop(r, b, mode, B, H, W, nT, noise);
+      record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
     } else if (prof.kernel_id >= 0) {
       // Profiling replay: HIP cannot report elapsed time between events recorded by graph
       // nodes (hipEventElapsedTime -> invalid handle), so the same launch sequence runs
@@ -1068,7 +1123,7 @@ class EngineT : public Engine {
       d.prof = &prof;
       d.zero = zero_page;
       prof.begin_pass();
-      record_loop(d, b, mode, B, H, W, nT, noise);
+      record_loop(d, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
       while (prof.ev.size() < 2 * prof.used) {
         hipEvent_t ev;
         HIP_OK(hipEventCreate(&ev));
@@ -1077,16 +1132,16 @@ class EngineT : public Engine {
       Run r = live(priv);
       r.prof = &prof;
       prof.begin_pass();
-      record_loop(r, b, mode, B, H, W, nT, noise);
+      record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
     } else {
-      GKey key{mkey, B, H, W, nT, noise};
+      GKey key{mkey, B, H, W, nT};
       auto it = graphs.find(key);
       if (it == graphs.end()) {
         Run r = live(priv);
         hipGraph_t g;
         HIP_OK(hipStreamBeginCapture(priv, hipStreamCaptureModeThreadLocal));
         try {
-          record_loop(r, b, mode, B, H, W, nT, noise);
+          record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
         } catch (...) {
           hipGraph_t dead;
           (void)hipStreamEndCapture(priv, &dead);
@@ -1114,7 +1169,7 @@ class EngineT : public Engine {
     Run r;
     r.dry = true;
     r.ar = &a;
-    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, nullptr, nullptr, 4);
+    unet->forward(r, nullptr, nullptr, B, H, W, nullptr, (const float*)1, nullptr, 4);
     return r.flops;
   }
   double encode_flops(int B) override {
@@ -1139,7 +1194,6 @@ class EngineT : public Engine {
   Arena arena;
   hipStream_t priv;
   hipEvent_t ev_in, ev_out;
-  uint64_t seed_host[2] = {0, 0};
   uint64_t noise_offset = 0;     // global index of image 0 (sharded runs)
   void* zero_page = nullptr;
 };

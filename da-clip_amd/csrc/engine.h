@@ -125,6 +125,7 @@ struct SdeSchedule {
   int T = 0;
   std::vector<float> thetas, sigmas, tcum, sbar;
   float dt = 0, max_sigma = 0;
+  double time_scale = 1.0;       // IRSDE.sample_scale = T / sample_T (sde_utils.py:88, 302)
   StepCoef coef(int t, int mode) const;
 };
 void compute_schedule(SdeSchedule& s, float max_sigma, int T, int schedule, float eps);

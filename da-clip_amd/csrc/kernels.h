@@ -108,8 +108,12 @@ size_t linear_attention_ws_floats(int B, int HW);
 void small_linear(const float* x, int ldx, const float* W, const float* b, float* y, int ldy,
                   int R, int I, int O, int pre_act, int post_act, const float* add, int add_ld,
                   int add_mod, hipStream_t st);
-// out[r, :nf] = SinusoidalPosEmb(t0 + dt * (r / B)) for r < R (module_util.py:41-48).
-void sinus_embedding(float* out, int R, int B, int nf, float t0, float dt, hipStream_t st);
+// out[r, :nf] = SinusoidalPosEmb(float((t0 + dt * (r / B)) * scale)) for r < R
+// (module_util.py:41-48; scale = IRSDE.sample_scale).
+void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, double scale,
+                     hipStream_t st);
+// p[0] = a, p[1] = b on the device, in stream order.
+void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st);
 // y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)
 void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st);
 

@@ -84,23 +84,36 @@ void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStre
   softmax_mul_kernel<<<R, 256, 0, st>>>(x, v, y, C);
 }
 
-// SinusoidalPosEmb (module_util.py:41-48) for R = n_t * B rows: row r uses time
-// t0 + dt * (r / B); emb = exp(k * -(ln(10000) / (half - 1))) in fp32.
-__global__ void sinus_kernel(float* out, int R, int B, int nf, float t0, float dt, float negemb) {
+// SinusoidalPosEmb (module_util.py:41-48) for R = n_t * B rows: row r uses the time
+// t = float((t0 + dt * (r / B)) * scale), i.e. the reference's python `t * self.sample_scale`
+// (sde_utils.py:197, 202, 302; a double) rounded once to the float32 time tensor
+// (DenoisingUNet_arch.py:120-121); emb = exp(k * -(ln(10000) / (half - 1))) in fp32.
+__global__ void sinus_kernel(float* out, int R, int B, int nf, double t0, double dt, double scale,
+                             float negemb) {
   const int half = nf / 2;
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= R * half) return;
   const int r = i / half, k = i - r * half;
-  const float t = t0 + dt * (float)(r / B);
+  const float t = (float)((t0 + dt * (double)(r / B)) * scale);
   const float a = t * expf((float)k * negemb);
   out[(size_t)r * nf + k] = sinf(a);
   out[(size_t)r * nf + half + k] = cosf(a);
 }
 
-void sinus_embedding(float* out, int R, int B, int nf, float t0, float dt, hipStream_t st) {
+void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, double scale,
+                     hipStream_t st) {
   const int half = nf / 2;
   const float negemb = (float)(-(std::log(10000.0) / (half - 1)));
-  sinus_kernel<<<(R * half + 255) / 256, 256, 0, st>>>(out, R, B, nf, t0, dt, negemb);
+  sinus_kernel<<<(R * half + 255) / 256, 256, 0, st>>>(out, R, B, nf, t0, dt, scale, negemb);
+}
+
+// Stage the loop's noise key on the device in stream order (kernel arguments, no host
+// staging buffer and no host synchronisation).
+__global__ void set_u64x2_kernel(uint64_t* p, uint64_t a, uint64_t b) {
+  if (threadIdx.x == 0) { p[0] = a; p[1] = b; }
+}
+void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st) {
+  set_u64x2_kernel<<<1, 64, 0, st>>>(p, a, b);
 }
 
 // --------------------------------------------------------------------------- UNet I/O

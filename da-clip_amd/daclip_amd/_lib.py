@@ -25,7 +25,7 @@ DAC_E_MISSING, DAC_E_KEY = -3, -2
 
 EXPORTS = ["dac_create", "dac_destroy", "dac_set_weight", "dac_finalize_weights",
            "dac_encode_image", "dac_encode_text", "dac_degradation_probs", "dac_unet_forward",
-           "dac_sde_schedule", "dac_sde_reverse",
+           "dac_sde_schedule", "dac_sde_set_time_scale", "dac_sde_reverse", "dac_build_id",
            "dac_set_noise_offset", "dac_posterior_step", "dac_unet_flops", "dac_encode_flops", "dac_profile_enable",
            "dac_profile_read", "dac_last_error"]
 
@@ -65,7 +65,9 @@ def lib() -> ctypes.CDLL:
         "dac_degradation_probs": (I, [P, P, P, I, I, I, P, P, P]),
         "dac_unet_forward": (I, [P, P, P, F, P, P, I, I, I, P, P]),
         "dac_sde_schedule": (I, [P, F, I, I, F, P, F]),
+        "dac_sde_set_time_scale": (I, [P, D]),
         "dac_sde_reverse": (I, [P, I, P, P, P, P, I, I, I, I, P, U64, P]),
+        "dac_build_id": (ctypes.c_char_p, []),
         "dac_set_noise_offset": (I, [P, U64]),
         "dac_posterior_step": (I, [P, I, P, P, P, P, I, I, P]),
         "dac_unet_flops": (D, [P, I, I, I]),
@@ -138,6 +140,28 @@ class Handle:
 
     def stream(self):
         return _stream(self.device)
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over csrc/* in byte order of the names, then the public
+    header: the value the Makefile bakes into dac_build_id() (da-clip_amd/Makefile)."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*")), key=lambda p: os.path.basename(p).encode())
+    files.append(os.path.join(os.path.dirname(pkg), "include", "daclip_hip.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """{"build_id": the loaded library's id, "source_hash": this tree's, "matches": bool}."""
+    bid = lib().dac_build_id().decode()
+    src = source_hash()
+    return {"build_id": bid, "source_hash": src, "matches": bid.split(" ")[0] == src}
 
 
 def exports_present(names: Sequence[str] = EXPORTS):

@@ -131,10 +131,10 @@ class IRSDE:
             if noises is not None:
                 nz = noises[:T].to(dev, torch.float32).contiguous()
             B, _, H, W = x.shape
-            if self.sample_scale != 1.0:
-                raise NotImplementedError("sample_T != T with the native loop")
             with torch.cuda.device(dev):
                 self._sync_schedule(h)
+                # the model sees t * sample_scale (sde_utils.py:266, 302)
+                h.check(_lib.lib().dac_sde_set_time_scale(h.h, float(self.sample_scale)), "time_scale")
                 self.seed += 1
                 h.check(_lib.lib().dac_set_noise_offset(h.h, int(self.image_offset)), "noise_offset")
                 h.check(_lib.lib().dac_sde_reverse(h.h, mode, _lib._ptr(x), _lib._ptr(mu_d),

@@ -123,7 +123,11 @@ int dac_sde_schedule(dac_handle* h, float max_sigma, int T, int schedule, float 
 /* Full reverse loop t = T..1 in place on x_inout [B,3,H,W] with mu = LQ [B,3,H,W].
  * noise: NULL -> device Philox N(0,1) keyed by (seed, step, element); else [T,B,3,H,W]
  * fp32 device tensor, slice i consumed at step t = T - i (parity mode). Captured once per
- * (B,H,W,T,mode) as a hipGraph and replayed. */
+ * (B,H,W,T,mode, which contexts / noise are given) as a hipGraph and replayed; injected
+ * noise is copied into a handle-owned buffer first, so the caller may free or reuse it.
+ * text_ctx NULL skips the prompt embedding (DenoisingUNet_arch.py:133-137); image_ctx NULL
+ * makes every SpatialTransformer's attn2 a self-attention (attention.py:174), which, as in
+ * the reference, requires context_dim == channels at those levels (DAC_E_ARG otherwise). */
 int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu,
                     const float* text_ctx, const float* image_ctx, int B, int H, int W, int T,
                     const float* noise, uint64_t seed, void* stream);
@@ -133,6 +137,12 @@ int dac_sde_reverse(dac_handle* h, int mode, float* x_inout, const float* mu,
  * `first_image` reproduces exactly the noise that image receives in an unsharded batch
  * (results are independent of the world size). Default 0. */
 int dac_set_noise_offset(dac_handle* h, uint64_t first_image);
+
+/* Time fed to the model at step t: t * scale, with scale = IRSDE.sample_scale = T / sample_T
+ * (utils/sde_utils.py:86-88, 266, 302: noise_fn(x, t, self.sample_scale)). Default 1. The
+ * product is formed in double and rounded once to float32, like the reference's python float
+ * becoming torch.tensor([time]) (DenoisingUNet_arch.py:120-121). */
+int dac_sde_set_time_scale(dac_handle* h, double scale);
 
 /* One sampler update given the model output: x <- step(x, eps, t, z); x, eps, mu, z are
  * [B,3,H,W] fp32 and n = B*3*H*W elements (must be a multiple of 3). */
@@ -152,6 +162,11 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
                      double* bytes_per_launch);
 
 const char* dac_last_error(dac_handle* h);
+
+/* Build provenance baked in at compile time: "<sha256 of the library sources>[:16] git=<HEAD>"
+ * (da-clip_amd/Makefile). The Python side recomputes the source hash from the tree, so a run
+ * can prove which sources the loaded library was built from. */
+const char* dac_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,11 @@ f32 = np.float32
 
 
 class IRSDE:
-    def __init__(self, max_sigma=50, T=100, schedule="cosine", eps=0.005):
+    def __init__(self, max_sigma=50, T=100, schedule="cosine", eps=0.005, sample_T=-1):
+        # sde_utils.py:84-89: the schedule is built over sample_T steps and the model is called
+        # at t * sample_scale, sample_scale = T / sample_T.
+        self.sample_scale = T / sample_T if sample_T > 0 else 1.0
+        T = sample_T if sample_T > 0 else T
         self.T = T
         self.max_sigma = max_sigma / 255 if max_sigma >= 1 else max_sigma
         ms = self.max_sigma
@@ -76,12 +80,12 @@ class IRSDE:
         T = T or self.T
         x = xt.copy()
         for i, t in enumerate(range(T, 0, -1)):
-            x = self.posterior_step(x, self.model(x, self.mu, float(t), **ctx), t, noises[i])
+            x = self.posterior_step(x, self.model(x, self.mu, t * self.sample_scale, **ctx), t, noises[i])
         return x
 
     def reverse_sde(self, xt, noises, T=None, **ctx):
         T = T or self.T
         x = xt.copy()
         for i, t in enumerate(range(T, 0, -1)):
-            x = self.sde_step(x, self.model(x, self.mu, float(t), **ctx), t, noises[i])
+            x = self.sde_step(x, self.model(x, self.mu, t * self.sample_scale, **ctx), t, noises[i])
         return x

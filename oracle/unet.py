@@ -78,7 +78,9 @@ def spatial_transformer(sd, p, x, ctx):
     q = p + "transformer_blocks.0."
     ln = lambda n, t: F.layer_norm(t, sd[q + n + ".weight"], sd[q + n + ".bias"])
     x = cross_attention(sd, q + "attn1.", ln("norm1", x), ln("norm1", x), heads) + x
-    x = cross_attention(sd, q + "attn2.", ln("norm2", x), ctx, heads) + x
+    # attn2: cross-attention on the context, or self-attention when none is given (:174).
+    xn2 = ln("norm2", x)
+    x = cross_attention(sd, q + "attn2.", xn2, xn2 if ctx is None else ctx, heads) + x
     hdn = F.linear(ln("norm3", x), sd[q + "ff.net.0.proj.weight"], sd[q + "ff.net.0.proj.bias"])
     a, gate = np.split(hdn, 2, axis=-1)
     x = F.linear(a * F.gelu(gate), sd[q + "ff.net.2.weight"], sd[q + "ff.net.2.bias"]) + x

@@ -132,6 +132,97 @@ def gen_sde():
                         psnr=np.float64(psnr))
 
 
+HEADLINE_IMAGE = "/root/reference/images/00006.jpg"      # a real 256x256 LQ photo
+HEADLINE_T = 100
+
+
+def headline_noise(shape_lq):
+    """Injected noises of the headline fixture (regenerated by the tests, never stored):
+    noise_state draw [1,3,H,W] and the T per-step draws [T,1,3,H,W]."""
+    n0 = synth.synth_noise(shape_lq, seed=71, tag="hl_noise_state")
+    steps = synth.synth_noise((HEADLINE_T,) + tuple(shape_lq), seed=72, tag="hl_steps")
+    return n0, steps
+
+
+def gen_headline():
+    """The benchmarked configuration pinned end to end on a real image (predict.py:58-91):
+    PIL-decoded 256x256 RGB -> /255 (float64, as predict.py:64) -> clip_transform (PIL
+    restatement, daclip_amd.preprocess; torchvision is absent) -> reference DaCLIP ViT-B/32
+    encode_image(control=True) -> reference noise_state + T=100 reverse_posterior of the
+    reference ConditionalUNet (nf=64) with injected noise -> tensor2img. Synthetic seeded
+    weights (seed 0) for both networks; fp32 CPU, i.e. the reference CPU path."""
+    from PIL import Image
+    from daclip_amd.preprocess import clip_transform
+    rgb = np.asarray(Image.open(HEADLINE_IMAGE).convert("RGB"))
+    image = rgb / 255.0                                              # predict.py:64 (float64)
+    img4clip = clip_transform(image).unsqueeze(0).numpy()
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    ic, dc = d.encode_image(T(img4clip), control=True)
+    ic, dc = ic.float(), dc.float()
+    lq = torch.tensor(image, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0)   # predict.py:73-75
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    load(m, seed=0)
+    sde = ref_utils.IRSDE(max_sigma=50, T=HEADLINE_T, schedule="cosine", eps=0.005, device="cpu")
+    sde.set_model(m)
+    n0, steps = headline_noise(tuple(lq.shape))
+    with NoiseInjector([n0]):
+        noisy = sde.noise_state(lq)
+    sde.set_mu(lq)
+    with NoiseInjector(list(steps)):
+        out = sde.reverse_posterior(noisy, text_context=dc, image_context=ic).numpy()
+    out_u8 = ref_utils.tensor2img(T(out.copy()).squeeze())
+    lq_u8 = ref_utils.tensor2img(lq.squeeze())
+    np.savez_compressed(os.path.join(HERE, "headline_256_t100.npz"), rgb_u8=rgb, img4clip=img4clip,
+                        image_context=ic.numpy(), degra_context=dc.numpy(), out=out, out_u8=out_u8,
+                        lq_u8=lq_u8, psnr_out_vs_lq=np.float64(ref_utils.calculate_psnr(out_u8, lq_u8)))
+
+
+def gen_variants():
+    """Two sampler / context variants of the reference, 16x16 / 32x32:
+    * sample_T != T: IRSDE(T=100, sample_T=50) -> 50-entry schedule and the model called at
+      t * sample_scale = 2t (sde_utils.py:84-89, 297-313), posterior loop with injected noise;
+    * image_context=None: every SpatialTransformer's attn2 becomes self-attention over
+      norm2(x) (attention.py:174). That only runs when context_dim equals the channels of
+      every SpatialTransformer level, so this UNet is nf=64, ch_mult [1,2,4,4], context 256."""
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    load(m, seed=0)
+    sde = ref_utils.IRSDE(max_sigma=50, T=100, sample_T=50, schedule="cosine", eps=0.005, device="cpu")
+    sde.set_model(m)
+    b, h, w = 1, 16, 16
+    lq = synth.synth_images(b, h, w, seed=81)
+    tc = synth.synth_noise((b, 512), seed=3, tag="text") * 0.5
+    ic = synth.synth_noise((b, 512), seed=4, tag="image") * 0.5
+    x0 = lq + synth.synth_noise((b, 3, h, w), seed=82, tag="st_noisy") * (50 / 255)
+    steps = synth.synth_noise((50, b, 3, h, w), seed=83, tag="st_steps")
+    sde.set_mu(T(lq))
+    with NoiseInjector(list(steps)):
+        out = sde.reverse_posterior(T(x0), text_context=T(tc), image_context=T(ic)).numpy()
+    out_s = {"st_lq": lq, "st_x0": x0, "st_tc": tc, "st_ic": ic, "st_steps": steps, "st_out": out,
+             "st_thetas": sde.thetas.numpy(), "st_dt": np.float32(sde.dt.item())}
+
+    cfg = dict(in_nc=3, out_nc=3, nf=64, ch_mult=[1, 2, 4, 4], context_dim=256,
+               use_degra_context=True, use_image_context=True)
+    m = ConditionalUNet(**cfg).eval()
+    spec = load(m, seed=1)
+    b, h, w = 2, 32, 32
+    xt = synth.synth_noise((b, 3, h, w), seed=84, tag="sc_xt") * 0.3 + 0.5
+    mu = synth.synth_images(b, h, w, seed=85)
+    tc = synth.synth_noise((b, 256), seed=86, tag="sc_text") * 0.5
+    out_s.update(sc_xt=xt, sc_mu=mu, sc_tc=tc,
+                 sc_fwd=m(T(xt), T(mu), 31.0, text_context=T(tc), image_context=None).numpy(),
+                 sc_fwd_notext=m(T(xt), T(mu), 7.0).numpy())
+    sde = ref_utils.IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005, device="cpu")
+    sde.set_model(m)
+    sde.set_mu(T(mu))
+    steps = synth.synth_noise((3, b, 3, h, w), seed=87, tag="sc_steps")
+    with NoiseInjector(list(steps)):
+        out_s["sc_loop3"] = sde.reverse_posterior(T(xt), T=3, text_context=T(tc)).numpy()
+    out_s["sc_steps"] = steps
+    np.savez_compressed(os.path.join(HERE, "sampler_variants.npz"), **out_s)
+    json.dump({k: list(v) for k, v in spec.items()}, open(os.path.join(HERE, "selfctx_state_spec.json"), "w"))
+
+
 def _daclip(vision, text, embed):
     d = DaCLIP(CLIP(embed_dim=embed, vision_cfg=vision, text_cfg=text)).eval()
     load(d, seed=0)
@@ -269,7 +360,8 @@ def gen_img_metrics():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "text", "wild", "modules", "img"]
     fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
-               text=gen_text, wild=gen_wild, modules=gen_modules, img=gen_img_metrics)
+               text=gen_text, wild=gen_wild, modules=gen_modules, img=gen_img_metrics,
+               headline=gen_headline, variants=gen_variants)
     for w in which:
         print("generating", w, flush=True)
         fns[w]()

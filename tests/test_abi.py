@@ -55,3 +55,13 @@ def test_config_struct_matches_header():
         assert decl.startswith("int "), decl
         names += [re.sub(r"\[.*\]", "", n).strip() for n in decl[4:].split(",")]
     assert [f[0] for f in _lib.DacConfig._fields_] == names
+
+
+def test_build_id_matches_sources():
+    """The library carries the hash of the sources it was built from (Makefile); a stale
+    build (sources edited after `make`) is caught here, before any GPU run."""
+    from daclip_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libdaclip_hip.so not built")
+    info = _lib.build_info()
+    assert info["matches"], info

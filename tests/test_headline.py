@@ -1,0 +1,104 @@
+"""The benchmarked configuration (256x256, T=100 posterior, ViT-B/32 DA-CLIP + nf=64 UNet)
+pinned end to end against the reference itself, run on a real image in the fixture builder
+(tests/golden/make_golden.py gen_headline: predict.py:58-91 on images/00006.jpg with seeded
+weights and injected noise). The HIP path restores B=8 copies through the captured graph loop.
+
+North-star bar: restored output within 1e-3 dB PSNR of the reference CPU path. The fixture
+has no ground truth, so PSNR is taken against the LQ input (as the reference's predict flow
+would be scored on an LQ-only image). With seeded random weights the restoration saturates
+(most pixels clamp to 0 or 255 in tensor2img), so the float output is compared as well.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B = 8
+# Seeds of the injected noises, as in make_golden.py headline_noise().
+NOISE_STATE = dict(seed=71, tag="hl_noise_state")
+STEPS = dict(seed=72, tag="hl_steps")
+T_STEPS = 100
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+def record(name, **kv):
+    """Measured values go to stdout and, on a GPU box, to gpurun_out/headline_metrics.jsonl."""
+    print(name, json.dumps(kv))
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "headline_metrics.jsonl"), "a") as f:
+            f.write(json.dumps({"test": name, **kv}) + "\n")
+
+
+@pytest.fixture(scope="module")
+def headline(golden):
+    from daclip_amd import synth
+    g = golden("headline_256_t100.npz")
+    lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0)   # predict.py:73-75
+    n0 = torch.from_numpy(synth.synth_noise(tuple(lq.shape), **NOISE_STATE))
+    steps = torch.from_numpy(synth.synth_noise((T_STEPS,) + tuple(lq.shape), **STEPS))
+    return g, lq, n0, steps
+
+
+def restore(dtype, g, lq, n0, steps, unet_sd):
+    """predict.py:63-86 on the HIP path for B copies of the fixture image."""
+    from daclip_amd import arch
+    from daclip_amd.open_clip import DaCLIP
+    from daclip_amd.unet import ConditionalUNet
+    from daclip_amd.sde import IRSDE
+    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=dtype, with_text=False)
+    clip.load_synthetic(seed=0)
+    img = torch.from_numpy(g["img4clip"]).cuda().expand(B, -1, -1, -1).contiguous()
+    ic, dc = clip.encode_image(img, control=True)
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype=dtype)
+    unet.load_state_dict(unet_sd)
+    sde = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+    sde.set_model(unet)
+    lqb = lq.cuda().expand(B, -1, -1, -1).contiguous()
+    noisy = sde.noise_state(lqb, noise=n0.cuda().expand(B, -1, -1, -1))
+    sde.set_mu(lqb)
+    z = steps.cuda().expand(-1, B, -1, -1, -1).contiguous()
+    out = sde.reverse_posterior(noisy, noises=z, text_context=dc, image_context=ic)
+    torch.cuda.synchronize()
+    return ic.cpu().numpy(), dc.cpu().numpy(), out.cpu().numpy()
+
+
+def check(name, g, ic, dc, out, ctx_tol, out_tol):
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    assert rel(ic[0], g["image_context"][0]) < ctx_tol
+    assert rel(dc[0], g["degra_context"][0]) < ctx_tol
+    for b in range(1, B):                               # every copy restores identically
+        assert np.array_equal(out[b], out[0]), b
+    ref = g["out"][0]
+    r = rel(out[0], ref)
+    u8 = tensor2img(torch.from_numpy(out[0]))
+    lq_u8 = g["lq_u8"]
+    d_psnr = calculate_psnr(u8, lq_u8) - calculate_psnr(g["out_u8"], lq_u8)
+    unsat = (ref > 0) & (ref < 1)
+    record(name, ctx_rel=max(rel(ic[0], g["image_context"][0]), rel(dc[0], g["degra_context"][0])),
+           out_rel=r, delta_psnr_db=d_psnr, psnr_vs_ref_u8=calculate_psnr(u8, g["out_u8"]),
+           u8_mismatch=float(np.mean(u8 != g["out_u8"])), unsaturated_frac=float(unsat.mean()),
+           unsat_max_abs=float(np.abs(out[0] - ref)[unsat].max()))
+    assert abs(d_psnr) < 1e-3                           # north-star bar
+    assert r < out_tol
+
+
+def test_headline_fp32_matches_reference(headline, unet_sd):
+    g, lq, n0, steps = headline
+    ic, dc, out = restore("fp32", g, lq, n0, steps, unet_sd)
+    check("headline_fp32", g, ic, dc, out, ctx_tol=1e-4, out_tol=1e-3)
+
+
+def test_headline_bf16_matches_reference(headline, unet_sd):
+    g, lq, n0, steps = headline
+    ic, dc, out = restore("bf16", g, lq, n0, steps, unet_sd)
+    check("headline_bf16", g, ic, dc, out, ctx_tol=5e-2, out_tol=1.0)
