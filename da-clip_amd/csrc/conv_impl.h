@@ -90,7 +90,8 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
     const int k = kt * BKE + slot * VE;
     const bool kv = k < a.K;
     int kpos = k / a.Cin;
-    const int ci = k - kpos * a.Cin;
+    int ci = k - kpos * a.Cin;
+    if (a.cwrap && ci >= a.cwrap) ci -= a.cwrap;
     const int kh = kpos / KW, kw = kpos - (kpos / KW) * KW;
     const bool from1 = ci < a.C1;
 #pragma unroll
@@ -359,10 +360,12 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     if constexpr (KH == 7 && sizeof(T) == 2) {
       // Row-tap layout (kernel row padded to 8 taps, Cin = 8 = one 16-byte vector): K tile kt
       // is kernel row kh = kt, and logical slot s of a pixel row is tap kw = s (s = 7: zero).
+      // Split-precision weights (cwrap): K tiles KH..2KH-1 are the lo rows of kernel rows 0..KH-1.
+      const int kr = (a.cwrap && kt >= KH) ? kt - KH : kt;
 #pragma unroll
       for (int j = 0; j < AG; ++j) {
         const int kw = a_ls[j];
-        const int ih = a_ih[j] + kt, iw = a_iw[j] + kw;
+        const int ih = a_ih[j] + kr, iw = a_iw[j] + kw;
         const char* src = zero;
         if (kv && kw < KW && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
           src = reinterpret_cast<const char*>(x1 + (size_t)(a_pix[j] + ih * a.Ws + iw) * a.ld1);
@@ -380,7 +383,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
       return;
     }
     const int kpos = k0 / a.Cin;                 // wave-uniform (Cin % BKE == 0)
-    const int ci0 = k0 - kpos * a.Cin;
+    int ci0 = k0 - kpos * a.Cin;
+    if (a.cwrap && ci0 >= a.cwrap) ci0 -= a.cwrap;   // split-precision weights (cwrap % BKE == 0)
     const int kh = kpos / KW, kw = kpos - (kpos / KW) * KW;
 #pragma unroll
     for (int j = 0; j < AG; ++j) {
@@ -1155,7 +1159,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     }
   }
   if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
-    if (a.Cin == 8 && a.K == 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {
+    if (a.Cin == 8 && a.K == (a.cwrap ? 2 : 1) * 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {
       const int Mg = a.B * a.Ho * a.Wo;
       dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, 1);
       conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P, EPI_ALL><<<g, 512, 0, st>>>(a);
@@ -1168,7 +1172,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     const bool epi_min = (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cout % (16 / (int)sizeof(T)) == 0 &&
                          a.ldy % (16 / (int)sizeof(T)) == 0 && (!a.res1 || a.ldr1 % (16 / (int)sizeof(T)) == 0) &&
                          (!a.res2 || a.ldr2 % (16 / (int)sizeof(T)) == 0);
-    if (v2ok && RW > 0 && a.w_bstride == 0 && epi_min) {
+    if (v2ok && RW > 0 && a.w_bstride == 0 && epi_min && a.cwrap == 0) {
       if (g_conv3_force > 0) {
         if (conv3i_launch<T>(g_conv3_force, a, st)) return;
       } else if (g_conv3_force < 0) {

@@ -14,6 +14,53 @@
 
 namespace dac {
 
+// ============================================================================= precision probe
+// Debug aid for locating where bf16 storage costs accuracy, fp32 handles only (off by default):
+// DAC_EMU_W / DAC_EMU_A are bit masks of UNet roles whose weights (at packing) / outputs (after
+// each kernel) are rounded to bf16, emulating the bf16 engine one part at a time.
+enum Role : int { R_INIT = 1, R_RB = 2, R_SAMP = 4, R_LA = 8, R_ST = 16, R_FINAL = 32, R_FIN_RB = 64,
+                  R_MID = 128, R_OTHER = 256 };
+static int env_mask(const char* n) {
+  const char* v = getenv(n);
+  return v ? (int)strtol(v, nullptr, 0) : 0;
+}
+static int emu_w() { static const int m = env_mask("DAC_EMU_W"); return m; }
+static int emu_a() { static const int m = env_mask("DAC_EMU_A"); return m; }
+static thread_local int g_role = R_OTHER;
+struct RoleScope {
+  int prev;
+  explicit RoleScope(int r) : prev(g_role) { g_role = r; }
+  ~RoleScope() { g_role = prev; }
+};
+// UNet weight key -> role (DenoisingUNet_arch.py module names).
+static int key_role(const std::string& k) {
+  auto has = [&](const char* s) { return k.find(s) != std::string::npos; };
+  if (k.rfind("init_conv", 0) == 0) return R_INIT;
+  if (k.rfind("final_conv", 0) == 0) return R_FINAL;
+  if (k.rfind("final_res_block", 0) == 0) return R_FIN_RB;
+  if (k.rfind("mid_", 0) == 0) return R_MID;
+  if (has(".fn.fn.to_qkv") || has(".fn.fn.to_out")) return R_LA;
+  if (has(".fn.fn.")) return R_ST;
+  if (has("block1") || has("block2") || has("res_conv") || has(".mlp.")) return R_RB;
+  if ((k.rfind("downs.", 0) == 0 && has(".3.")) || (k.rfind("ups.", 0) == 0 && has(".3."))) return R_SAMP;
+  return R_OTHER;
+}
+template <typename T>
+static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
+// DAC_EMU_WSKIP: comma-separated key substrings whose weights stay fp32 under DAC_EMU_W.
+static bool emu_w_key(const std::string& k) {
+  if (!(emu_w() & key_role(k))) return false;
+  static const std::string skip = getenv("DAC_EMU_WSKIP") ? getenv("DAC_EMU_WSKIP") : "";
+  size_t a = 0;
+  while (a < skip.size()) {
+    size_t b = skip.find(',', a);
+    if (b == std::string::npos) b = skip.size();
+    if (b > a && k.find(skip.substr(a, b - a)) != std::string::npos) return false;
+    a = b + 1;
+  }
+  return true;
+}
+
 // ============================================================================= weights
 const HostW* WStore::get(const std::string& key, std::vector<int64_t> shape) {
   auto it = m.find(key);
@@ -54,16 +101,79 @@ uint16_t f2bf_host(float f) {
   return (uint16_t)(u >> 16);
 }
 
+static float bf2f_host(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+// The bf16 neighbour of h one step toward f (h != f, both finite).
+static uint16_t bf_toward(uint16_t h, float f) {
+  const float v = bf2f_host(h);
+  const bool up = f > v;
+  if (v == 0.f) return up ? 0x0001 : 0x8001;
+  return (uint16_t)(((v > 0.f) == up) ? h + 1 : h - 1);
+}
+// Weight rounding to bf16. Round-to-nearest leaves a per-layer systematic error (the same
+// every step and pixel); by default (DAC_WROUND=1; 0 = plain RNE) each (output row, input channel) group of `taps`
+// kernel taps is rounded so that its sum is kept (greedy flips of the taps closest to the
+// rounding midpoint), which removes the error's response to smooth inputs.
+static int wround_mode() {
+  static const int m = getenv("DAC_WROUND") ? env_mask("DAC_WROUND") : 1;   // default: sum-keeping
+  return m;
+}
+static std::vector<uint16_t> quantize_bf16(const std::vector<float>& v, int taps, int cin) {
+  std::vector<uint16_t> h(v.size());
+  for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host(v[i]);
+  if (wround_mode() != 1 || taps < 2) return h;
+  const size_t rows = v.size() / ((size_t)taps * cin);
+  std::vector<size_t> idx(taps);
+  std::vector<char> used(taps);
+  for (size_t o = 0; o < rows; ++o)
+    for (int c = 0; c < cin; ++c) {
+      double r = 0;
+      for (int t = 0; t < taps; ++t) {
+        idx[t] = (o * taps + t) * cin + c;
+        used[t] = 0;
+        r += (double)v[idx[t]] - bf2f_host(h[idx[t]]);
+      }
+      for (int it = 0; it < taps; ++it) {
+        int best = -1;
+        double br = std::fabs(r);
+        for (int t = 0; t < taps; ++t) {
+          const float w = v[idx[t]];
+          const uint16_t q = h[idx[t]];
+          if (used[t] || bf2f_host(q) == w || !std::isfinite(w)) continue;
+          const double nr = r + (double)bf2f_host(q) - bf2f_host(bf_toward(q, w));
+          if (std::fabs(nr) < br) { br = std::fabs(nr); best = t; }
+        }
+        if (best < 0) break;
+        const uint16_t q = h[idx[best]], q2 = bf_toward(q, v[idx[best]]);
+        r += (double)bf2f_host(q) - bf2f_host(q2);
+        h[idx[best]] = q2;
+        used[best] = 1;
+      }
+    }
+  return h;
+}
+
 template <typename T>
 struct Packer {
   DevPool& pool;
   WStore& ws;
   static constexpr int VE = sizeof(T) == 2 ? 8 : 4;
 
-  const void* upload_T(const std::vector<float>& v) {
-    if (sizeof(T) == 4) return pool.upload(v.data(), v.size() * 4);
-    std::vector<uint16_t> h(v.size());
-    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host(v[i]);
+  // v: packed [rows][taps][cin] weights.
+  const void* upload_T(const std::vector<float>& v, const std::string& key = "", int taps = 1, int cin = 1) {
+    if (cin <= 1) cin = (int)v.size(), taps = 1;
+    if (sizeof(T) == 4) {
+      if (!emu_w_key(key)) return pool.upload(v.data(), v.size() * 4);
+      const std::vector<uint16_t> h = quantize_bf16(v, taps, cin);
+      std::vector<float> q(v.size());
+      for (size_t i = 0; i < v.size(); ++i) q[i] = bf2f_host(h[i]);
+      return pool.upload(q.data(), q.size() * 4);
+    }
+    const std::vector<uint16_t> h = quantize_bf16(v, taps, cin);
     return pool.upload(h.data(), h.size() * 2);
   }
   const float* f32(const std::string& key, std::vector<int64_t> shape) {
@@ -99,11 +209,46 @@ struct Packer {
         for (int y = 0; y < kh; ++y)
           for (int x = 0; x < kw; ++x)
             p[(((size_t)o * kh + y) * kws + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
-    cw.w = upload_T(p);
+    cw.w = upload_T(p, key, kh * kws, cw.cin);
     return cw;
   }
   ConvW linear(const std::string& key, int O, int I, const std::string& bkey = "") {
     return conv(key, O, I, 1, 1, bkey, true);
+  }
+  // Split-precision weights (bf16 handles; fp32 handles keep plain fp32 weights): hi = RNE(w),
+  // lo = RNE(w - hi), packed [O][kh][kws][hi cin | lo cin], or, for the 7x7 row-tap layout
+  // (kwp > kw), [O][hi rows | lo rows]. The layer then computes A.hi + A.lo in one fp32
+  // accumulator: weight error ~2^-17 relative instead of bf16's 2^-9.
+  ConvW conv_dual(const std::string& key, int O, int C, int kh, int kw, const std::string& bkey = "",
+                  int kwp = 0) {
+    if (sizeof(T) == 4) return conv(key, O, C, kh, kw, bkey, false, kwp);
+    ConvW cw;
+    cw.cout = O; cw.cin_real = C; cw.cin = pad_to(C, VE); cw.kh = kh; cw.kw = kw;
+    cw.kwp = kwp > kw ? kwp : 0;
+    cw.dual = 1;
+    const int kws = cw.kwp ? cw.kwp : kw;
+    const HostW* w = ws.get(key, {O, C, kh, kw});
+    if (!bkey.empty()) cw.b = f32(bkey, {O});
+    if (!w) return cw;
+    const size_t per = (size_t)kh * kws * cw.cin;                // one precision part of a row
+    std::vector<uint16_t> h((size_t)O * 2 * per, 0);
+    for (int o = 0; o < O; ++o)
+      for (int c = 0; c < C; ++c)
+        for (int y = 0; y < kh; ++y)
+          for (int x = 0; x < kw; ++x) {
+            const float v = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
+            const uint16_t hi = f2bf_host(v), lo = f2bf_host(v - bf2f_host(hi));
+            const size_t tap = (size_t)y * kws + x;
+            if (cw.kwp) {
+              h[(size_t)o * 2 * per + tap * cw.cin + c] = hi;
+              h[(size_t)o * 2 * per + per + tap * cw.cin + c] = lo;
+            } else {
+              h[(size_t)o * 2 * per + tap * 2 * cw.cin + c] = hi;
+              h[(size_t)o * 2 * per + tap * 2 * cw.cin + cw.cin + c] = lo;
+            }
+          }
+    cw.w = pool.upload(h.data(), h.size() * 2);
+    return cw;
   }
   // Row-concatenation of several [Oi][I] linears (q | k | v) into one GEMM.
   ConvW concat(const std::vector<std::string>& keys, int O, int I) {
@@ -116,7 +261,7 @@ struct Packer {
       if (!w) { ok = false; continue; }
       p.insert(p.end(), w->v.begin(), w->v.end());
     }
-    if (ok) cw.w = upload_T(p);
+    if (ok) cw.w = upload_T(p, keys[0]);
     return cw;
   }
   // GEGLU proj [2F][I] (+bias): rows reordered so each 32-row group holds 16 "x" rows then
@@ -135,7 +280,7 @@ struct Packer {
                 p.begin() + (size_t)r * I);
       pb[r] = b->v[src];
     }
-    cw.w = upload_T(p);
+    cw.w = upload_T(p, key);
     cw.b = (const float*)pool.upload(pb.data(), pb.size() * 4);
     return cw;
   }
@@ -157,6 +302,18 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.Ho = (Hin + 2 * pad - cw.kh) / stride + 1;
   a.Wo = (Win + 2 * pad - cw.kw) / stride + 1;
   a.Cout = cw.cout; a.K = cw.kh * (cw.kwp ? cw.kwp : cw.kw) * cw.cin; a.w = cw.w; a.bias = cw.b;
+  a.cwrap = 0;
+  if (cw.dual) {
+    // [hi | lo] along K: the input is read twice (ConvArgs::cwrap).
+    a.K *= 2;
+    if (cw.kwp) {
+      a.cwrap = 1;                                   // 7x7 row-tap layout: kernel rows wrap
+    } else if (x2 == nullptr) {
+      a.Cin = 2 * cw.cin; a.x2 = x1; a.ld2 = ld1; a.C1 = cw.cin;   // second copy via x2
+    } else {
+      a.Cin = 2 * cw.cin; a.cwrap = cw.cin;          // [x1 | x2 | x1 | x2]
+    }
+  }
   a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
@@ -171,13 +328,14 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     return;
   }
   if (!cw.w) throw Error(DAC_E_STATE, "conv weight not loaded");
-  if (a.Cin % (16 / (int)sizeof(T)) || (x2 == nullptr && C1 < a.Cin))
+  if (a.Cin % (16 / (int)sizeof(T)) || (a.x2 == nullptr && a.C1 < a.Cin))
     throw Error(DAC_E_ARG, "conv: bad channel layout");
   if (timed) {
     if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
     HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
   }
   conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+  emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
   if (timed) {
     HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
     p->used++;
@@ -199,10 +357,17 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
 }
 
 template <typename T>
+static void emu_round(const Run& r, void* y, int ld, size_t rows, int C) {
+  if (sizeof(T) == 4 && !r.dry && (emu_a() & g_role))
+    round_bf16_rows(reinterpret_cast<float*>(y), ld, rows, C, r.st);
+}
+
+template <typename T>
 static void ln(Run& r, const void* x, int ldx, void* y, int ldy, const void* res, int ldr,
                const float* g, const float* b, int rows, int C, float eps) {
   if (r.dry) return;
   layernorm<T>(x, ldx, y, ldy, res, ldr, g, b, rows, C, eps, r.st);
+  emu_round<T>(r, y, ldy, (size_t)rows, C);
 }
 
 // ============================================================================= schedule
@@ -311,7 +476,7 @@ struct UNetNet {
     for (int i = 0; i < depth; ++i) levels.push_back({nf * m[i], nf * m[i + 1]});
   }
 
-  RB load_rb(Packer<T>& P, const std::string& p, int din, int dout) {
+  RB load_rb(Packer<T>& P, const std::string& p, int din, int dout, bool dual_res = false) {
     RB rb;
     rb.din = din; rb.dout = dout;
     rb.mw = P.f32(p + "mlp.1.weight", {2 * dout, tdim});
@@ -320,7 +485,8 @@ struct UNetNet {
     rb.c2 = P.conv(p + "block2.proj.weight", dout, dout, 3, 3);
     if (din != dout) {
       rb.has_res = true;
-      rb.res = P.conv(p + "res_conv.weight", dout, din, 1, 1);
+      rb.res = dual_res ? P.conv_dual(p + "res_conv.weight", dout, din, 1, 1)
+                        : P.conv(p + "res_conv.weight", dout, din, 1, 1);
     }
     rb.ss_off = ss_total;
     ss_total += 2 * dout;
@@ -379,8 +545,11 @@ struct UNetNet {
     if (degra) prompt = P.f32("prompt", {1, tdim});
     // bf16: [xt | mu] has 6 (-> 8) channels = one 16-byte vector per pixel, so a K tile of 64
     // elements is 8 neighbouring pixels of one input row (kernel row padded to 8 taps).
-    init_conv = P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", false,
-                       sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0);
+    // init_conv, final_conv and final_res_block.res_conv keep split-precision weights in bf16
+    // handles: their bf16 rounding error alone moved the T=100 restore by up to ~1e-3 dB
+    // (measured with the DAC_EMU_* probe); together they are ~1.4 % of the FLOPs.
+    init_conv = P.conv_dual("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "",
+                            sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0);
     if (half) {
       half_down = P.conv("downsample.weight", nf, nf, 4, 4, "downsample.bias");
       half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias");
@@ -424,8 +593,8 @@ struct UNetNet {
     mid1 = load_rb(P, "mid_block1.", mid, mid);
     mid_attn = load_attn(P, "mid_attn.", mid, imgctx);
     mid2 = load_rb(P, "mid_block2.", mid, mid);
-    fin = load_rb(P, "final_res_block.", 2 * nf, nf);
-    final_conv = P.conv("final_conv.weight", cfg.out_nc, nf, 3, 3, "final_conv.bias");
+    fin = load_rb(P, "final_res_block.", 2 * nf, nf, /*dual_res=*/true);
+    final_conv = P.conv_dual("final_conv.weight", cfg.out_nc, nf, 3, 3, "final_conv.bias");
   }
 
   // ----------------------------------------------------------------- per-call tables
@@ -504,6 +673,7 @@ struct UNetNet {
   }
 
   const void* linattn(Run& r, const LA& la, const void* x, int C, int B, int H, int W) {
+    RoleScope rs(g_role == R_MID ? R_MID : R_LA);
     const size_t M = (size_t)B * H * W;
     if (C == 64 || C == 128) {
       // Fused front half (linattn.hip): LN + to_qkv + context in one pass over x; q is
@@ -514,6 +684,8 @@ struct UNetNet {
       r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32;
       if (!r.dry)
         linear_attention_fused<T>(x, la.gpre, la.qkv.w, q, la.wout, weff, B, H * W, C, ws, r.st);
+      emu_round<T>(r, q, 128, M, 128);
+      emu_round<T>(r, weff, 128, (size_t)B * C, 128);
       // to_out (per-image weights) with its LayerNorm and the Residual in the epilogue.
       ConvW wo;
       wo.w = weff; wo.b = la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
@@ -547,6 +719,7 @@ struct UNetNet {
 
   const void* sptrans(Run& r, const ST& s, const void* x, int C, int B, int H, int W,
                       const float* cc) {
+    RoleScope rs(g_role == R_MID ? R_MID : R_ST);
     const int L = H * W;
     const size_t M = (size_t)B * L;
     T* xn = r.alloc<T>(M * C);
@@ -556,6 +729,7 @@ struct UNetNet {
     // (mean, rstd) [B][32][2].
     float* stats = r.alloc<float>((size_t)B * 32 * (32 * 3 + 2));
     if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
+    emu_round<T>(r, gn, C, M, C);
     T* hh = r.alloc<T>(M * C);
     conv_call<T>(r, s.pin, gn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, Epi());
     T* a = r.alloc<T>(M * C);
@@ -565,6 +739,7 @@ struct UNetNet {
     T* o = r.alloc<T>(M * C);
     r.flops += 4.0 * B * (double)L * L * C;     // QK^T and PV
     if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, 0.17677669529663687f, r.st);
+    emu_round<T>(r, o, C, M, C);
     T* h2 = r.alloc<T>(M * C);
     Epi e;
     e.res1 = hh; e.ldr1 = C;
@@ -627,6 +802,7 @@ struct UNetNet {
     T* xin = r.alloc<T>(M0 * 8);
     if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
     T* x0 = r.alloc<T>(M0 * nf);
+    RoleScope rs_init(R_INIT);
     conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
     std::vector<std::pair<const void*, int>> hs;
     const void* cur = x0;
@@ -640,10 +816,12 @@ struct UNetNet {
     for (int i = 0; i < depth; ++i) {
       const auto [din, dout] = levels[i];
       Level& L = downs[i];
+      g_role = R_RB;
       cur = resblock(r, L.b1, cur, din, nullptr, 0, B, h, w, ss);
       hs.push_back({cur, din});
       cur = resblock(r, L.b2, cur, din, nullptr, 0, B, h, w, ss);
       cur = attn(r, L.at, cur, din, B, h, w, cc);
+      g_role = R_SAMP;
       hs.push_back({cur, din});
       if (i != depth - 1) {
         T* y = r.alloc<T>((size_t)B * (h / 2) * (w / 2) * dout);
@@ -657,6 +835,7 @@ struct UNetNet {
       }
     }
     const int mid = levels.back().second;
+    g_role = R_MID;
     cur = resblock(r, mid1, cur, mid, nullptr, 0, B, h, w, ss);
     cur = attn(r, mid_attn, cur, mid, B, h, w, cc);
     cur = resblock(r, mid2, cur, mid, nullptr, 0, B, h, w, ss);
@@ -665,10 +844,12 @@ struct UNetNet {
       const auto [din, dout] = levels[i];
       Level& L = ups[j];
       auto sk = hs.back(); hs.pop_back();
+      g_role = R_RB;
       cur = resblock(r, L.b1, cur, dout, sk.first, sk.second, B, h, w, ss);
       sk = hs.back(); hs.pop_back();
       cur = resblock(r, L.b2, cur, dout, sk.first, sk.second, B, h, w, ss);
       cur = attn(r, L.at, cur, dout, B, h, w, cc);
+      g_role = R_SAMP;
       if (i != 0) {
         T* y = r.alloc<T>((size_t)B * (2 * h) * (2 * w) * din);
         conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 1, 1, 1, y, din, Epi());
@@ -686,7 +867,9 @@ struct UNetNet {
       cur = xu;
       h = Hp; w = Wp;
     }
+    g_role = R_FIN_RB;
     cur = resblock(r, fin, cur, nf, x0, nf, B, h, w, ss);
+    g_role = R_FINAL;
     conv_call<T>(r, final_conv, cur, nf, nf, nullptr, 0, B, h, w, 0, 1, 1, out, ldo, Epi());
   }
 };

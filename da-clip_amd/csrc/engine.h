@@ -60,6 +60,10 @@ struct ConvW {
   const float* b = nullptr;
   int cout = 0, cin = 0, cin_real = 0, kh = 1, kw = 1;
   int kwp = 0;   // > kw: taps of a kernel row padded to kwp with zero weights (K = kh*kwp*cin)
+  // 1: split-precision weights [hi | lo] along K (doubles the executed MFMA work of the layer),
+  // see ConvArgs::cwrap. Used in bf16 handles for the layers whose weight rounding error is
+  // systematic enough to move the restored image.
+  int dual = 0;
 };
 
 // ----------------------------------------------------------------------------- run context

@@ -40,11 +40,17 @@ struct ConvArgs {
   // 180-185). Requires one N tile covering Cout.
   const float* ln_g;
   float ln_eps;
+  // Split-precision ("dual") weights of a layer whose bf16 rounding error is systematic enough
+  // to move the restored image (engine.cpp Packer::conv dual): W = W_hi + W_lo, stored as the
+  // K range [hi | lo] over the input read twice. cwrap > 0: input channel ci >= cwrap reads
+  // channel ci - cwrap (two-source layers; then split by C1 as usual); for the 7x7 row-tap
+  // layout, kernel row kt >= KH reads row kt - KH.
+  int cwrap;
 };
 
 // Shapes served by the weight-stationary 3x3 kernel (conv_impl.h conv3w_kernel, bf16 only).
 inline bool conv3w_ok(const ConvArgs& a) {
-  return a.Cin == 64 && a.Cout == 64 && a.K == 576 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
+  return a.Cin == 64 && a.Cout == 64 && a.K == 576 && a.cwrap == 0 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
          !a.ln_g && (a.act == ACT_NONE || a.act == ACT_SILU) && a.Wo >= 64 && a.Wo % 64 == 0 &&
          (a.C1 >= a.Cin || a.C1 % 32 == 0) && a.ldy % 8 == 0 && a.ld1 % 8 == 0 &&
          (a.C1 >= a.Cin || a.ld2 % 8 == 0) && (!a.res1 || a.ldr1 % 8 == 0) && (!a.res2 || a.ldr2 % 8 == 0);
@@ -112,6 +118,8 @@ void small_linear(const float* x, int ldx, const float* W, const float* b, float
 // (module_util.py:41-48; scale = IRSDE.sample_scale).
 void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, double scale,
                      hipStream_t st);
+// Precision analysis: y[r*ld + c] = float(bf16(y[r*ld + c])) for r < rows, c < C.
+void round_bf16_rows(float* y, int ld, size_t rows, int C, hipStream_t st);
 // p[0] = a, p[1] = b on the device, in stream order.
 void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st);
 // y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)

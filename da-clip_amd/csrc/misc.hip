@@ -107,6 +107,19 @@ void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, dou
   sinus_kernel<<<(R * half + 255) / 256, 256, 0, st>>>(out, R, B, nf, t0, dt, scale, negemb);
 }
 
+// Precision analysis (DAC_EMU_A, engine.cpp): round fp32 rows to bf16 in place, as a bf16
+// store followed by a load would (round to nearest even).
+__global__ void round_bf16_kernel(float* y, int ld, size_t rows, int C) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * C) return;
+  float* p = y + (i / C) * ld + i % C;
+  *p = (float)(bf16)(*p);
+}
+void round_bf16_rows(float* y, int ld, size_t rows, int C, hipStream_t st) {
+  const size_t n = rows * C;
+  if (n) round_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(y, ld, rows, C);
+}
+
 // Stage the loop's noise key on the device in stream order (kernel arguments, no host
 // staging buffer and no host synchronisation).
 __global__ void set_u64x2_kernel(uint64_t* p, uint64_t a, uint64_t b) {

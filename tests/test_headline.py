@@ -99,6 +99,11 @@ def test_headline_fp32_matches_reference(headline, unet_sd):
 
 
 def test_headline_bf16_matches_reference(headline, unet_sd):
+    """The benchmarked mode. Measured: dPSNR 2.9e-4 dB, 55.9 dB against the reference's uint8
+    output, float max-rel 3.2e-4 (bf16 weights with sum-keeping rounding; split-precision
+    init_conv / final_conv / final_res_block.res_conv, engine.cpp)."""
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
     g, lq, n0, steps = headline
     ic, dc, out = restore("bf16", g, lq, n0, steps, unet_sd)
-    check("headline_bf16", g, ic, dc, out, ctx_tol=5e-2, out_tol=1.0)
+    check("headline_bf16", g, ic, dc, out, ctx_tol=2e-2, out_tol=8e-4)
+    assert calculate_psnr(tensor2img(torch.from_numpy(out[0])), g["out_u8"]) > 50.0

@@ -1,7 +1,7 @@
 """Parity of the HIP path (through the C ABI) against the reference's golden fixtures and the
 numpy oracle. Tolerances: fp32 mode uses exact-f32 MFMA, so differences come only from
-summation order (rel 1e-4 on a forward); bf16 mode (perf path) is checked against a looser
-bound that reflects bf16 storage (rel 5e-2)."""
+summation order (rel 1e-4 on a forward); bf16 mode (perf path) bounds are ~2x the measured
+error of bf16 storage (forward: measured max-rel 5.9e-3..6.4e-3, bound 1.5e-2)."""
 import numpy as np
 import pytest
 import torch
@@ -44,7 +44,8 @@ def test_unet_forward_bf16_close(golden, unets, tag):
     g = golden(f"unet_fwd_nf64_{tag}.npz")
     out = unets["bf16"](T(g["xt"]), T(g["mu"]), float(g["t"]), text_context=T(g["text_context"]),
                         image_context=T(g["image_context"])).cpu().numpy()
-    assert rel(out, g["out"]) < 5e-2
+    print(f"bf16 forward {tag}: rel {rel(out, g['out']):.3e}")
+    assert rel(out, g["out"]) < 1.5e-2
 
 
 def test_unet_batch_invariance_and_determinism_256(unets):
@@ -75,7 +76,8 @@ def test_unet_forward_256_fp32_vs_oracle(unets, unet_sd):
     out = unets["fp32"](T(x), T(mu), 77.0, text_context=T(tc), image_context=T(ic)).cpu().numpy()
     assert rel(out, ref) < 1e-4
     outb = unets["bf16"](T(x), T(mu), 77.0, text_context=T(tc), image_context=T(ic)).cpu().numpy()
-    assert rel(outb, ref) < 5e-2
+    print(f"bf16 forward 256: rel {rel(outb, ref):.3e}")
+    assert rel(outb, ref) < 1.5e-2
 
 
 def test_posterior_loop_fp32_matches_reference(golden, unets):
@@ -106,8 +108,9 @@ def test_posterior_loop_fp32_matches_reference(golden, unets):
 
 
 def test_posterior_loop_bf16_psnr(golden, unets):
-    """The bf16 perf path on the same T=100 fixture: PSNR delta vs the reference output is
-    reported, bounded loosely (bf16 storage; measured 2e-3 dB, 44.6 dB vs the reference)."""
+    """The bf16 perf path on the same T=100 fixture, held to the north-star bar: |dPSNR| vs the
+    reference < 1e-3 dB (measured -2.6e-4 dB; 57.1 dB against the reference's uint8 output,
+    float max-rel 2.8e-4)."""
     from daclip_amd.sde import IRSDE
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     g = golden("posterior_loop_16x16.npz")
@@ -118,8 +121,11 @@ def test_posterior_loop_bf16_psnr(golden, unets):
                                 image_context=T(g["image_context"]))
     u8 = tensor2img(out[0])
     gt = tensor2img(torch.from_numpy(g["lq"][0]))
-    assert abs(calculate_psnr(u8, gt) - calculate_psnr(g["out_u8"], gt)) < 0.05
-    assert calculate_psnr(u8, g["out_u8"]) > 35.0
+    print(f"bf16 loop 16x16: dPSNR {calculate_psnr(u8, gt) - calculate_psnr(g['out_u8'], gt):.3e} dB, "
+          f"vs ref {calculate_psnr(u8, g['out_u8']):.2f} dB, rel {rel(out.cpu().numpy(), g['out']):.3e}")
+    assert abs(calculate_psnr(u8, gt) - calculate_psnr(g["out_u8"], gt)) < 1e-3
+    assert calculate_psnr(u8, g["out_u8"]) > 50.0
+    assert rel(out.cpu().numpy(), g["out"]) < 6e-4
 
 
 def test_python_loop_matches_native_loop(golden, unets):
@@ -189,7 +195,9 @@ def test_daclip_encode_matches_reference(golden, name, dt):
     m = DaCLIP(v, t, dtype=dt)
     m.load_synthetic(seed=0)
     ic, dc = m.encode_image(T(g["img"]), control=True)
-    tol = 1e-4 if dt == "fp32" else 5e-2
+    print(f"encode {name} {dt}: rel {rel(ic.cpu().numpy(), g['image_context']):.3e} / "
+          f"{rel(dc.cpu().numpy(), g['degra_context']):.3e}")
+    tol = 1e-4 if dt == "fp32" else 2e-2      # bf16: measured 5.8e-3 .. 8.6e-3
     assert rel(ic.cpu().numpy(), g["image_context"]) < tol
     assert rel(dc.cpu().numpy(), g["degra_context"]) < tol
 
