@@ -112,27 +112,37 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
           Mma<T>::run(s[mi], ka, qf[g][ks]);
         }
       }
-      // Online softmax over keys for this lane's query column.
+      // Online softmax over keys for this lane's query column, in the log2 domain: the running
+      // max is kept pre-scaled by c = scale * log2(e), so each probability is one FMA and one
+      // v_exp_f32: p = 2^(s * c - m) (c > 0, so the max of raw scores is the max of scaled).
+      const float c = scale * 1.4426950408889634f;
       float tmax = -INFINITY;
+      if (k0 + KT <= L) {                        // whole tile valid (every UNet shape)
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + mi * 16 + lg * 4 + r;
-          const float v = key < L ? s[mi][r] * scale : -INFINITY;
-          s[mi][r] = v;
-          tmax = fmaxf(tmax, v);
-        }
+          for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[mi][r]);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + mi * 16 + lg * 4 + r;
+            if (key >= L) s[mi][r] = -INFINITY;
+            tmax = fmaxf(tmax, s[mi][r]);
+          }
+      }
       tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
       tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(mrun[g], tmax);
-      const float corr = sizeof(T) == 2 ? __expf(mrun[g] - mnew) : expf(mrun[g] - mnew);
+      const float mnew = fmaxf(mrun[g], tmax * c);
+      const float corr = sizeof(T) == 2 ? __builtin_amdgcn_exp2f(mrun[g] - mnew) : exp2f(mrun[g] - mnew);
       float psum = 0.f;
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = sizeof(T) == 2 ? __expf(s[mi][r] - mnew) : expf(s[mi][r] - mnew);
+          const float a = fmaf(s[mi][r], c, -mnew);
+          const float p = sizeof(T) == 2 ? __builtin_amdgcn_exp2f(a) : exp2f(a);
           s[mi][r] = p;
           psum += p;
         }

@@ -676,25 +676,15 @@ struct UNetNet {
     RoleScope rs(g_role == R_MID ? R_MID : R_LA);
     const size_t M = (size_t)B * H * W;
     if (C == 64 || C == 128) {
-      // Fused front half (linattn.hip): LN + to_qkv + context in one pass over x; q is
-      // written already softmaxed and scaled, so to_out is a plain per-image-weight GEMM.
-      T* q = r.alloc<T>(M * 128);
+      // Fused (linattn.hip): context pass over x, then one apply pass x -> y (LN, q projection
+      // and softmax, per-image to_out, its LayerNorm and the Residual).
       T* weff = r.alloc<T>((size_t)B * C * 128);
       float* ws = r.alloc<float>(linear_attention_fused_ws_floats(B, H * W));
-      r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32;
-      if (!r.dry)
-        linear_attention_fused<T>(x, la.gpre, la.qkv.w, q, la.wout, weff, B, H * W, C, ws, r.st);
-      emu_round<T>(r, q, 128, M, 128);
-      emu_round<T>(r, weff, 128, (size_t)B * C, 128);
-      // to_out (per-image weights) with its LayerNorm and the Residual in the epilogue.
-      ConvW wo;
-      wo.w = weff; wo.b = la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
       T* y = r.alloc<T>(M * C);
-      Epi eo;
-      eo.w_bstride = (long long)C * 128;
-      eo.ln_g = la.gout; eo.ln_eps = 1e-5f;
-      eo.res1 = x; eo.ldr1 = C;
-      conv_call<T>(r, wo, q, 128, 128, nullptr, 0, B, H, W, 0, 1, 0, y, C, eo);
+      r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32 + 2.0 * M * 128 * C;
+      if (!r.dry)
+        linear_attention_fused<T>(x, la.gpre, la.qkv.w, la.wout, la.bout, la.gout, weff, y, B, H * W, C, ws, r.st);
+      emu_round<T>(r, y, C, M, C);
       return y;
     }
     T* xn = r.alloc<T>(M * C);

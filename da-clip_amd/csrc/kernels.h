@@ -100,12 +100,14 @@ void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal,
 template <typename T>
 void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
                            float* ws, hipStream_t st);
-// Fused PreNorm + to_qkv + context (C in {64, 128}): writes q = softmax_d(q) * 32^-0.5 to
-// qout [B*HW][128] and W_eff to weff; ws: linear_attention_fused_ws_floats(B, HW) floats.
+// Whole LinearAttention block, Residual(PreNorm(LinearAttention)) (module_util.py:27-33,
+// 89-97, 157-185), for C in {64, 128}: y = x + LN_out(to_out(ctx^T softmax_d(q))) with the
+// to_out bias and gain; weff: [B][C][128] scratch (per-image to_out weights), ws:
+// linear_attention_fused_ws_floats(B, HW) floats.
 template <typename T>
-void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, void* qout,
-                            const float* wout, void* weff, int B, int HW, int C, float* ws,
-                            hipStream_t st);
+void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, const float* wout,
+                            const float* bout, const float* gout, void* weff, void* y, int B, int HW,
+                            int C, float* ws, hipStream_t st);
 size_t linear_attention_fused_ws_floats(int B, int HW);
 size_t linear_attention_ws_floats(int B, int HW);
 

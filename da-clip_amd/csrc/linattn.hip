@@ -12,6 +12,7 @@
 //   la_weff   : W_eff[b][c][h*32+d] = sum_e Wout[c][h*32+e] ctx[h][d][e] / sum[h*32+d] / HW
 // The apply step is then the to_out GEMM on softmax_d(q)*scale with per-image W_eff
 // (conv.hip, amode = 1) — (Wout ctx^T) q = Wout (ctx^T q).
+#include <algorithm>
 #include <type_traits>
 
 #include "common.h"
@@ -207,17 +208,23 @@ template void linear_attention_weff<bf16>(const void*, const float*, void*, int,
 
 
 // =====================================================================================
-// Fused LinearAttention front half (PreNorm + to_qkv + context), C in {64, 128}:
+// Fused LinearAttention (PreNorm + to_qkv + context + to_out + LayerNorm + Residual), C in
+// {64, 128}, as two passes over x (the k-softmax over all pixels forces a full-image reduction
+// between them):
 //   la_proj_ctx : per (pixel chunk, image) block, one wave per head, 64-pixel tiles (32 for
 //                 fp32): x tile -> channel LayerNorm in registers (module_util.py:77-86) ->
-//                 LDS -> q|k|v projection on MFMA (weights in registers for bf16) ->
-//                 q: softmax over the head's 32 channels * 32^-0.5, written out (the to_out
-//                 GEMM reads it) ; k: online per-channel max with rescaling of the running
-//                 context / sums ; exp(k - m) and v staged transposed -> ctx += P V^T (MFMA).
+//                 LDS -> k|v projection on MFMA (weights in registers for bf16) ->
+//                 k: online per-channel max with rescaling of the running context / sums ;
+//                 exp(k - m) and v straight from the accumulators -> ctx += P V^T (MFMA).
 //   la_combine  : rescales every chunk partial to the global channel max and sums them in
 //                 fixed order -> the same [ctx | sum] layout la_weff consumes.
-// HBM traffic per image: read x once, write q (128 ch), instead of x->xn->qkv(384 ch)->k,v.
-// The chunking depends only on HW (la_chunks), so results stay batch- and shard-invariant.
+//   la_weff     : per-image to_out weights W_eff = Wout ctx^T / sum / HW.
+//   la_apply    : x tile -> LayerNorm -> q projection (MFMA) -> softmax over each head's 32
+//                 channels * 32^-0.5 -> out = W_eff q (MFMA, W_eff staged in LDS) -> + bias ->
+//                 LayerNorm over C (to_out.1) -> + x (Residual) -> y.
+// HBM traffic per image: x read twice, y written once (2 * HW * C elements in, HW * C out),
+// instead of x -> xn -> qkv (384 ch) -> k, v and a q round trip. The chunking depends only
+// on HW (la_chunks), so results stay batch- and shard-invariant.
 constexpr int LA_FPART = 4096 + 256;   // ctx | sum | max
 
 // Reductions over the 16 lanes of a DPP row (the lanes holding one MFMA C-tile row): quad
@@ -286,7 +293,7 @@ template <> struct OpPack<float> {
 
 template <typename T, int C>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 64 ? 2 : 1, 2))) la_proj_ctx(const T* __restrict__ x, const float* __restrict__ g,
-                                                   const T* __restrict__ w, T* __restrict__ qo,
+                                                   const T* __restrict__ w,
                                                    float* __restrict__ part, int HW, int nc, int CH,
                                                    float eps) {
   using K = LaCfg<T, C>;
@@ -379,8 +386,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
   for (int t0 = p0; t0 < p1; t0 += TP) {
     const bool more = t0 + TP < p1;
     if (more) xload(t0 + TP);
-    // ---- projection, in two phases to bound live accumulators: q (col tiles 0,1) first,
-    // then k|v (2..5). acc[pt][jt] = xn[pt rows] . W[jt cols]
+    // ---- k|v projection (col tiles 2..5). acc[pt][jt] = xn[pt rows] . W[jt cols]
     const char* xt = sx + buf * K::XT;
     auto project = [&](auto& acc, int j0, auto nj) __attribute__((always_inline)) {
       constexpr int NJ = decltype(nj)::value;
@@ -402,35 +408,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
         }
       }
     };
-    f32x4 aq[PT][2];
-    project(aq, 0, std::integral_constant<int, 2>{});
-    // ---- q: softmax over the head's 32 channels (16 lanes x 2 tiles) per pixel row.
-    T* sq = reinterpret_cast<T*>(sP);                     // [TP][32], aliases P (wave-local)
-#pragma unroll
-    for (int pt = 0; pt < PT; ++pt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float a0 = aq[pt][0][r], a1 = aq[pt][1][r];
-        const float m = row16_max(fmaxf(a0, a1));
-        a0 = exp_t<T>(a0 - m);
-        a1 = exp_t<T>(a1 - m);
-        const float inv = rcp_t<T>(row16_sum(a0 + a1));
-        const int px = pt * 16 + lg * 4 + r;
-        sq[px * 32 + lr] = from_f<T>(a0 * inv * 0.17677669529663687f);
-        sq[px * 32 + 16 + lr] = from_f<T>(a1 * inv * 0.17677669529663687f);
-      }
-    wave_sync_lds();
-    {
-      constexpr int CPP = 32 / VE;                        // 16-byte chunks per pixel
-#pragma unroll
-      for (int k = 0; k < TP * CPP / 64; ++k) {
-        const int ci = lane + k * 64, px = ci / CPP, cc = (ci % CPP) * VE;
-        if (t0 + px < p1)
-          *reinterpret_cast<u32x4*>(qo + ((size_t)b * HW + t0 + px) * 128 + h * 32 + cc) =
-              *reinterpret_cast<const u32x4*>(sq + px * 32 + cc);
-      }
-    }
-    wave_sync_lds();
     f32x4 acc[PT][4];                                     // k (0,1) | v (2,3)
     project(acc, 2, std::integral_constant<int, 4>{});
     // ---- k: tile max per channel over valid pixels, online rescale.
@@ -494,7 +471,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) Mma<T>::run(cacc[i][j], fp[i][kk], fv[j][kk]);
-    wave_sync_lds();                                      // P/V reads done before next q writes
+    wave_sync_lds();                                      // sm reads done before the next tile
     // ---- next tile: normalise the prefetched pixels into the other buffer.
     if (more) xstore(buf ^ 1);
     __syncthreads();
@@ -557,26 +534,265 @@ size_t linear_attention_fused_ws_floats(int B, int HW) {
   return (size_t)B * nc * LA_FPART + (size_t)B * LA_PART;
 }
 
+// --------------------------------------------------------------------------------------
+// la_apply: the back half, one wave per 16-pixel tile, no block barrier after the weight
+// staging (waves walk their own tiles). Orientation is chosen so that no operand needs a
+// transpose:
+//   q^T[qch][px] = Wq[qch][:] . LN(x)[px][:]   A = Wq rows (LDS), B = the x tile loaded
+//                                              straight from HBM in the MFMA B layout and
+//                                              LayerNorm'd in registers (xor shuffles)
+//   softmax over each head's 32 q channels      rows of the accumulators: registers + lanes
+//   out^T[ch][px] = W_eff[ch][:] . q^T[:][px]   B = the softmaxed accumulators repacked in
+//                                              registers (the k order they come in is baked
+//                                              into W_eff's LDS columns), A = W_eff rows
+//                                              permuted (la_perm) so each lane ends with the
+//                                              very channels of its pixel it loaded for the
+//                                              LayerNorm: the Residual comes from registers
+//   + bias, LayerNorm over C (to_out.1), * g, + x (Residual), 16-byte stores.
+// Row p = 16j + 4lg + r of a 64-channel half -> channel: bf16 32(j>>1) + 8lg + 4(j&1) + r
+// (x chunk ks = 2*half + (j>>1), element 4(j&1) + r); fp32 identity (ks = 4*half + j).
+template <typename T> DEV int la_perm(int p) {
+  if constexpr (sizeof(T) == 2) return 32 * (p >> 5) + 8 * ((p >> 2) & 3) + 4 * ((p >> 4) & 1) + (p & 3);
+  else return p;
+}
+
+// Grid (nb, B): block i of an image takes its i-th contiguous share of the image's 16-pixel
+// tiles (the last one partial when HW % 16 != 0, e.g. the Wild-IR half-resolution levels),
+// nb sized so the whole grid is resident at once (no half-empty second round).
+template <typename T, int C>
+__global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const float* __restrict__ g,
+                                                const T* __restrict__ w, const T* __restrict__ weff,
+                                                const float* __restrict__ bout, const float* __restrict__ gout,
+                                                T* __restrict__ y, int HW, float eps) {
+  constexpr int ES = sizeof(T), VE = TypeInfo<T>::VE, KSTEP = Mma<T>::KSTEP;
+  constexpr int KS = C / KSTEP;                           // q-projection k-steps
+  constexpr int KO = 128 / KSTEP;                         // out-GEMM k-steps
+  constexpr int NH = C / 64;                              // 64-channel output halves
+  constexpr int WROW = C * ES + 16, EROW = 128 * ES + 16; // LDS rows (+16 B)
+  constexpr int SMEM = 128 * WROW + C * EROW;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char* sq = smem;                                        // Wq [128][C]
+  char* sw = smem + 128 * WROW;                           // W_eff [C][128] permuted
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int b = blockIdx.y;
+  const int nt_img = (HW + 15) / 16;
+  const int p0 = (int)((long)blockIdx.x * nt_img / gridDim.x) * 16;
+  const int p1 = min(HW, (int)((long)(blockIdx.x + 1) * nt_img / gridDim.x) * 16);
+  if (p0 >= p1) return;
+  const T* xb = x + (size_t)b * HW * C;
+  T* yb = y + (size_t)b * HW * C;
+  {
+    // Wq = rows 0..127 of to_qkv. W_eff[b]: LDS row p of 64-half hf = channel hf*64 + perm(p);
+    // column k = 32s + 8*lg' + j holds q channel rho = 32s + (j < 4 ? 4lg' + j : 16 + 4lg' + j - 4)
+    // for bf16 (the order the repacked accumulators supply); natural order for fp32.
+    constexpr int CPRQ = C / VE, CPRE = 128 / VE;
+    for (int i = tid; i < 128 * CPRQ; i += 256) {
+      const int r = i / CPRQ, cc = (i % CPRQ) * VE;
+      *reinterpret_cast<u32x4*>(sq + r * WROW + cc * ES) = *reinterpret_cast<const u32x4*>(w + (size_t)r * C + cc);
+    }
+    const T* wb = weff + (size_t)b * C * 128;
+    for (int i = tid; i < C * CPRE; i += 256) {
+      const int p = i / CPRE, k0 = (i % CPRE) * VE;
+      const int ch = (p & ~63) + la_perm<T>(p & 63);
+      T* dst = reinterpret_cast<T*>(sw + p * EROW + k0 * ES);
+      if constexpr (ES == 2) {
+        const int s = k0 >> 5, l4 = ((k0 >> 3) & 3) * 4;
+#pragma unroll
+        for (int j = 0; j < VE; ++j) dst[j] = wb[(size_t)ch * 128 + 32 * s + (j < 4 ? l4 + j : 16 + l4 + j - 4)];
+      } else {
+        *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(wb + (size_t)ch * 128 + k0);
+      }
+    }
+  }
+  // This lane's LayerNorm gains (channels ks*KSTEP + lg*VE + j) and epilogue terms.
+  float gx[KS][VE];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int j = 0; j < VE; ++j) gx[ks][j] = g[ks * KSTEP + lg * VE + j];
+  __syncthreads();
+
+  const int ntile = (p1 - p0 + 15) / 16;
+  u32x4 xr[KS];
+  auto xload = [&](int t) {
+    const int px = p0 + t * 16 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      xr[ks] = px < p1 ? *reinterpret_cast<const u32x4*>(xb + (size_t)px * C + ks * KSTEP + lg * VE)
+                       : u32x4{0u, 0u, 0u, 0u};
+  };
+  int t = wv;
+  if (t < ntile) xload(t);
+  for (; t < ntile; t += 4) {
+    // The LDS weight fragments are loop-invariant; re-read them each tile instead of letting
+    // the compiler hoist ~128 VGPRs of them out of the loop (occupancy).
+    asm volatile("" ::: "memory");
+    // ---- LayerNorm of pixel lr (its C channels: KS*VE per lane x 4 lane groups).
+    float v[KS][VE];
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const T* e = reinterpret_cast<const T*>(&xr[ks]);
+#pragma unroll
+      for (int j = 0; j < VE; ++j) { v[ks][j] = to_f(e[j]); s += v[ks][j]; }
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.f / (float)C);
+    float qs = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < VE; ++j) { const float d = v[ks][j] - mean; qs += d * d; }
+    qs += __shfl_xor(qs, 16, 64);
+    qs += __shfl_xor(qs, 32, 64);
+    const float rstd = rsq_t<T>(qs * (1.f / (float)C) + eps);
+    u32x4 xf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      OpPack<T> pk;
+#pragma unroll
+      for (int j = 0; j < VE; ++j) pk.set(j, (v[ks][j] - mean) * rstd * gx[ks][j]);
+      xf[ks] = pk.get();
+    }
+    const int tcur = t;
+    if (t + 4 < ntile) xload(t + 4);                      // next tile in flight
+    // ---- q^T = Wq . xn^T : 8 tiles of 16 q channels.
+    f32x4 aq[8];
+#pragma unroll
+    for (int jt = 0; jt < 8; ++jt) aq[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int jt = 0; jt < 8; ++jt) {
+        const u32x4 fw = *reinterpret_cast<const u32x4*>(sq + (jt * 16 + lr) * WROW + (ks * KSTEP + lg * VE) * ES);
+        Mma<T>::run(aq[jt], fw, xf[ks]);
+      }
+    // ---- softmax over head hd = channels of tiles 2hd, 2hd+1 (rows 4lg + r on this lane).
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(aq[2 * hd][r], aq[2 * hd + 1][r]));
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      float sm = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        aq[2 * hd][r] = exp_t<T>(aq[2 * hd][r] - m);
+        aq[2 * hd + 1][r] = exp_t<T>(aq[2 * hd + 1][r] - m);
+        sm += aq[2 * hd][r] + aq[2 * hd + 1][r];
+      }
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      const float inv = rcp_t<T>(sm) * 0.17677669529663687f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { aq[2 * hd][r] *= inv; aq[2 * hd + 1][r] *= inv; }
+    }
+    // ---- repack as B fragments of the out GEMM (k = q channel).
+    u32x4 qf[KO];
+#pragma unroll
+    for (int s2 = 0; s2 < KO; ++s2) {
+      OpPack<T> pk;
+      if constexpr (ES == 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { pk.set(r, aq[2 * s2][r]); pk.set(4 + r, aq[2 * s2 + 1][r]); }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk.set(r, aq[s2][r]);
+      }
+      qf[s2] = pk.get();
+    }
+    // ---- out^T = W_eff . q^T
+    f32x4 acc[NH][4];
+#pragma unroll
+    for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[hf][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < KO; ++s2)
+#pragma unroll
+      for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const u32x4 fw = *reinterpret_cast<const u32x4*>(sw + (hf * 64 + j * 16 + lr) * EROW + (s2 * KSTEP + lg * VE) * ES);
+          Mma<T>::run(acc[hf][j], fw, qf[s2]);
+        }
+    // ---- epilogue: o[ks][jj] is channel ks*KSTEP + lg*VE + jj of pixel px, the element x
+    // arrived in (v[ks][jj] still holds it for the Residual).
+    const int px = p0 + tcur * 16 + lr;
+    float o[KS][VE];
+    float so = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int jj = 0; jj < VE; ++jj) {
+        const int hf = ES == 2 ? ks >> 1 : ks >> 2;
+        const int j = ES == 2 ? 2 * (ks & 1) + (jj >> 2) : ks & 3;
+        const int r = ES == 2 ? jj & 3 : jj;
+        o[ks][jj] = acc[hf][j][r] + bout[ks * KSTEP + lg * VE + jj];
+        so += o[ks][jj];
+      }
+    so += __shfl_xor(so, 16, 64);
+    so += __shfl_xor(so, 32, 64);
+    const float mo = so * (1.f / (float)C);
+    float qo = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int jj = 0; jj < VE; ++jj) { const float d = o[ks][jj] - mo; qo += d * d; }
+    qo += __shfl_xor(qo, 16, 64);
+    qo += __shfl_xor(qo, 32, 64);
+    const float ro = 1.f / sqrtf(qo * (1.f / (float)C) + 1e-5f);
+    if (px < p1) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float oo[VE];
+#pragma unroll
+        for (int jj = 0; jj < VE; ++jj)
+          oo[jj] = (o[ks][jj] - mo) * ro * gout[ks * KSTEP + lg * VE + jj] + v[ks][jj];
+        store_vec<T>(yb + (size_t)px * C + ks * KSTEP + lg * VE, oo);
+      }
+    }
+  }
+}
+
 template <typename T>
-void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, void* qout,
-                            const float* wout, void* weff, int B, int HW, int C, float* ws,
-                            hipStream_t st) {
+void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, const float* wout,
+                            const float* bout, const float* gout, void* weff, void* y, int B, int HW,
+                            int C, float* ws, hipStream_t st) {
   const int nc = la_chunks(B, HW), CH = la_chunk_px(HW, nc);
   float* part = ws;
   float* ctx = part + (size_t)B * nc * LA_FPART;
   if (C == 64)
-    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (T*)qout, part,
-                                                    HW, nc, CH, 1e-5f);
+    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
   else
-    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (T*)qout, part,
-                                                     HW, nc, CH, 1e-5f);
+    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
   la_combine<<<dim3((LA_PART + 31) / 32, B), 256, 0, st>>>(part, ctx, nc);
   la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, 1.f / (float)HW);
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
+      ncu = 256;
+  }
+  // Resident blocks per CU: 3 (C = 64, 3 waves / SIMD) or 2 (C = 128).
+  const int per_cu = (C == 64 ? 3 : 2) * (sizeof(T) == 2 ? 1 : 1);
+  int nb = (per_cu * ncu + B - 1) / B;
+  nb = std::max(1, std::min(nb, (HW + 63) / 64));
+  if (C == 64)
+    la_apply<T, 64><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                 (T*)y, HW, 1e-5f);
+  else
+    la_apply<T, 128><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                  (T*)y, HW, 1e-5f);
 }
 
-template void linear_attention_fused<float>(const void*, const float*, const void*, void*, const float*,
-                                            void*, int, int, int, float*, hipStream_t);
-template void linear_attention_fused<bf16>(const void*, const float*, const void*, void*, const float*,
-                                           void*, int, int, int, float*, hipStream_t);
+template void linear_attention_fused<float>(const void*, const float*, const void*, const float*, const float*,
+                                            const float*, void*, void*, int, int, int, float*, hipStream_t);
+template void linear_attention_fused<bf16>(const void*, const float*, const void*, const float*, const float*,
+                                           const float*, void*, void*, int, int, int, float*, hipStream_t);
 
 }  // namespace dac

@@ -144,12 +144,13 @@ class Handle:
 
 def source_hash() -> str:
     """sha256 (first 16 hex digits) over csrc/* in byte order of the names, then the public
-    header: the value the Makefile bakes into dac_build_id() (da-clip_amd/Makefile)."""
+    header and the Makefile: the value the Makefile bakes into dac_build_id()."""
     import glob
     import hashlib
     pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     files = sorted(glob.glob(os.path.join(pkg, "csrc", "*")), key=lambda p: os.path.basename(p).encode())
     files.append(os.path.join(os.path.dirname(pkg), "include", "daclip_hip.h"))
+    files.append(os.path.join(pkg, "Makefile"))
     h = hashlib.sha256()
     for f in files:
         with open(f, "rb") as fh:
