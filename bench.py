@@ -22,7 +22,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "restored images/sec @256x256, 100 IR-SDE steps; PSNR vs ref; 1/2/4/8 MI355X"
-MFMA_PEAK = {"bf16": 2500.0, "fp32": 157.3}       # dense TFLOP/s (MI355X_MICROARCH.md)
+MFMA_PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
@@ -58,7 +58,9 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="images per GPU (8; wild-ir 2)")
     p.add_argument("--res", type=int, default=None, help="resolution (256; wild-ir 512)")
     p.add_argument("--T", type=int, default=100)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                   help="bf16 (default); fp8 = e4m3 MX GEMMs for every conv/linear with Cin %% 64 == 0 "
+                        "(BASELINE configs[4]); fp32 = parity mode")
     p.add_argument("--kernel-id", type=int, default=312,
                    help="conv class timed for the roofline (kh*100 + variant; 312 = 3x3 interleaved-row v4 tiles)")
     p.add_argument("--no-cpu-baseline", action="store_true")

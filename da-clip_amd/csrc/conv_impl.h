@@ -326,12 +326,13 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   const T* wgt = reinterpret_cast<const T*>(a.w) + (batched ? tl.bz * a.w_bstride : 0);
 
   // This lane's rows: A row (wave*AG + j)*8 + lane/8, B row (wave*BG + j)*8 + lane/8.
-  int a_pix[AG], a_ih[AG], a_iw[AG], a_ls[AG];
+  int a_pix[AG], a_ih[AG], a_iw[AG], a_ls[AG], a_m[AG];
 #pragma unroll
   for (int j = 0; j < AG; ++j) {
     const int row = (wave * AG + j) * 8 + (lane >> 3);
     a_ls[j] = (lane & 7) ^ ((row >> 1) & 7);
     const int m = m0 + row;
+    a_m[j] = m;
     if (m < M) {
       const int b = m / HWo, r = m - b * HWo;
       const int oh = r / a.Wo, ow = r - oh * a.Wo;
@@ -369,6 +370,29 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
         const char* src = zero;
         if (kv && kw < KW && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
           src = reinterpret_cast<const char*>(x1 + (size_t)(a_pix[j] + ih * a.Ws + iw) * a.ld1);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < BG; ++j) {
+        const char* src = zero;
+        if (kv && b_row[j]) src = reinterpret_cast<const char*>(b_row[j] + k0 + b_ls[j] * VE);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(st + BM * 128 + (wave * BG + j) * 8 * 128),
+                                         16, 0, 0);
+      }
+      return;
+    }
+    if constexpr (KH == 1 && KW == 1 && S == 1 && P == 0) {
+      // Pointwise conv / linear (never upsampled, K = Cin): row m reads pixel m.
+      int ci0 = k0;
+      if (a.cwrap && ci0 >= a.cwrap) ci0 -= a.cwrap;
+      const bool from1 = ci0 < a.C1;
+      const char* xs = from1 ? reinterpret_cast<const char*>(x1 + ci0) : reinterpret_cast<const char*>(x2 + (ci0 - a.C1));
+      const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * sizeof(T);
+#pragma unroll
+      for (int j = 0; j < AG; ++j) {
+        const char* src = (kv && a_ih[j] >= 0) ? xs + (size_t)a_m[j] * ldb + a_ls[j] * 16 : zero;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                          (lds_void_t*)(st + (wave * AG + j) * 8 * 128), 16, 0, 0);
       }
@@ -942,6 +966,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 // 0 = v3 only, k > 0 = v4 configuration k of conv3i_launch.
 extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
+extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
@@ -1253,8 +1278,9 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       }
       __builtin_trap();                          // the engine only asks for these shapes
     }
-    if constexpr (KH == 1) if (g_conv2_force > 0) {
-      switch (g_conv2_force) {
+    const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho * a.Wo <= 1024) ? g_conv2_force32 : g_conv2_force;
+    if constexpr (KH == 1) if (f2 > 0) {
+      switch (f2) {
         case 1: DAC_V2(256, 128, 4, 2, 3, 512)
         case 2: DAC_V2(128, 128, 2, 2, 2, 256)
         case 3: DAC_V2(256, 128, 4, 2, 2, 512)
@@ -1269,6 +1295,16 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         case 8: DAC_V2(64, 128, 2, 2, 2, 256)
         case 9: DAC_V2(64, 64, 2, 2, 3, 256)
         case 10: DAC_V2(128, 64, 2, 2, 3, 256)
+        case 11: DAC_V2(64, 128, 2, 2, 3, 256)
+        case 12: DAC_V2(64, 128, 2, 2, 4, 256)
+        case 13:
+          if constexpr (sizeof(T) == 2)
+            if (minimal(64) && a.Cout % 128 == 0) {
+              dim3 g((Mg + 63) / 64, a.Cout / 128, gz);
+              conv2_kernel<T, 64, 128, 2, 2, 3, KH, KW, S, P, EPI_SWAP><<<g, 256, 0, st>>>(a);
+              return;
+            }
+          DAC_V2(64, 128, 2, 2, 3, 256)
         default: break;
       }
     }

@@ -157,11 +157,54 @@ static std::vector<uint16_t> quantize_bf16(const std::vector<float>& v, int taps
   return h;
 }
 
+// Host f32 -> OCP e4m3 (e4m3fn: bias 7, max 448, no infinities), round to nearest even,
+// saturating to +-448.
+static uint8_t f2e4m3_host(float f) {
+  const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+  const float a = std::fabs(f);
+  if (std::isnan(a)) return 0x7f;
+  if (a >= 464.f) return sign | 0x7e;
+  if (a < std::ldexp(1.f, -6)) {                       // subnormal: q * 2^-9
+    const int q = (int)std::nearbyint(a * 512.f);
+    return sign | (uint8_t)(q >= 8 ? 0x08 : q);
+  }
+  int e;
+  std::frexp(a, &e);                                   // a = m * 2^e, m in [0.5, 1)
+  int E = e - 1 + 7;
+  int q = (int)std::nearbyint((a / std::ldexp(1.f, e - 1) - 1.f) * 8.f);
+  if (q == 8) { q = 0; ++E; }
+  if (E > 15 || (E == 15 && q == 7)) return sign | 0x7e;
+  return sign | (uint8_t)(E << 3) | (uint8_t)q;
+}
+
 template <typename T>
 struct Packer {
   DevPool& pool;
   WStore& ws;
+  bool fp8 = false;                    // also build the e4m3 weights of every eligible layer
   static constexpr int VE = sizeof(T) == 2 ? 8 : 4;
+
+  // fp8 copy of a packed [O][K] weight (conv8.hip): K padded to a multiple of 128 with zeros,
+  // one E8M0 exponent per (row, 64-k block) chosen so the block's largest |w| / 2^e <= 448.
+  void make_fp8(ConvW& cw, const std::vector<float>& p, int O, int K) {
+    if (!fp8 || sizeof(T) != 2 || cw.cin % 64) return;
+    const int Kp = (K + 127) / 128 * 128;
+    std::vector<uint8_t> w8((size_t)O * Kp, 0), s8((size_t)O * (Kp / 64), 127);
+    for (int o = 0; o < O; ++o)
+      for (int b = 0; b < Kp / 64; ++b) {
+        float mx = 0.f;
+        for (int k = 64 * b; k < std::min(64 * b + 64, K); ++k) mx = std::max(mx, std::fabs(p[(size_t)o * K + k]));
+        int e = mx > 0.f ? (int)std::ceil(std::log2(mx / 448.f)) : 0;
+        e = std::min(126, std::max(-126, e));
+        s8[(size_t)o * (Kp / 64) + b] = (uint8_t)(127 + e);
+        const float inv = std::ldexp(1.f, -e);
+        for (int k = 64 * b; k < std::min(64 * b + 64, K); ++k)
+          w8[(size_t)o * Kp + k] = f2e4m3_host(p[(size_t)o * K + k] * inv);
+      }
+    cw.w8 = (const uint8_t*)pool.upload(w8.data(), w8.size());
+    cw.ws8 = (const uint8_t*)pool.upload(s8.data(), s8.size());
+    cw.kp8 = Kp;
+  }
 
   // v: packed [rows][taps][cin] weights.
   const void* upload_T(const std::vector<float>& v, const std::string& key = "", int taps = 1, int cin = 1) {
@@ -210,6 +253,7 @@ struct Packer {
           for (int x = 0; x < kw; ++x)
             p[(((size_t)o * kh + y) * kws + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
     cw.w = upload_T(p, key, kh * kws, cw.cin);
+    make_fp8(cw, p, O, kh * kws * cw.cin);
     return cw;
   }
   ConvW linear(const std::string& key, int O, int I, const std::string& bkey = "") {
@@ -261,7 +305,10 @@ struct Packer {
       if (!w) { ok = false; continue; }
       p.insert(p.end(), w->v.begin(), w->v.end());
     }
-    if (ok) cw.w = upload_T(p, keys[0]);
+    if (ok) {
+      cw.w = upload_T(p, keys[0]);
+      make_fp8(cw, p, cw.cout, I);
+    }
     return cw;
   }
   // GEGLU proj [2F][I] (+bias): rows reordered so each 32-row group holds 16 "x" rows then
@@ -281,6 +328,7 @@ struct Packer {
       pb[r] = b->v[src];
     }
     cw.w = upload_T(p, key);
+    make_fp8(cw, p, 2 * F, I);
     cw.b = (const float*)pool.upload(pb.data(), pb.size() * 4);
     return cw;
   }
@@ -321,7 +369,8 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   r.flops += fl;
   Profiler* p = r.prof;
-  const int cls = cw.kh * 100 + conv_variant(a, cw.kh, (int)sizeof(T));
+  const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
+  const int cls = cw.kh * 100 + (use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
   const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == cls);
   if (r.dry) {
     if (timed) p->used++;
@@ -334,7 +383,8 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
     HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
   }
-  conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+  if (use8) conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
+  else conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
   emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
   if (timed) {
     HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
@@ -1032,7 +1082,7 @@ struct VitNet {
 template <typename T>
 class EngineT : public Engine {
  public:
-  EngineT(int device, const dac_config& c) : dev(device), cfg(c) {
+  EngineT(int device, const dac_config& c, bool fp8w = false) : dev(device), cfg(c), fp8(fp8w) {
     HIP_OK(hipSetDevice(dev));
     HIP_OK(hipStreamCreateWithFlags(&priv, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
@@ -1063,6 +1113,7 @@ class EngineT : public Engine {
   void finalize(WStore& ws) override {
     HIP_OK(hipSetDevice(dev));
     Packer<T> P{pool, ws};
+    P.fp8 = fp8;
     if (unet) unet->load(P);
     if (vit) vit->load(P, ws);
     if (!ws.missing.empty()) {
@@ -1360,6 +1411,7 @@ class EngineT : public Engine {
 
   int dev;
   dac_config cfg;
+  bool fp8 = false;              // DAC_FP8 handle: e4m3 weights + conv8 for eligible layers
   bool ready = false;
   DevPool pool;
   std::unique_ptr<UNetNet<T>> unet;
@@ -1374,7 +1426,8 @@ class EngineT : public Engine {
 std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {
   if (dtype == DAC_F32) return std::make_unique<EngineT<float>>(device, cfg);
   if (dtype == DAC_BF16) return std::make_unique<EngineT<bf16>>(device, cfg);
-  throw Error(DAC_E_ARG, "dtype must be DAC_F32 or DAC_BF16");
+  if (dtype == DAC_FP8) return std::make_unique<EngineT<bf16>>(device, cfg, true);
+  throw Error(DAC_E_ARG, "dtype must be DAC_F32, DAC_BF16 or DAC_FP8");
 }
 
 template void conv_call<float>(Run&, const ConvW&, const void*, int, int, const void*, int, int,

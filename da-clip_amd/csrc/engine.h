@@ -64,6 +64,10 @@ struct ConvW {
   // see ConvArgs::cwrap. Used in bf16 handles for the layers whose weight rounding error is
   // systematic enough to move the restored image.
   int dual = 0;
+  // fp8 handles: e4m3 weights [cout][kp8] + E8M0 block exponents [cout][kp8 / 64] (conv8.hip).
+  const uint8_t* w8 = nullptr;
+  const uint8_t* ws8 = nullptr;
+  int kp8 = 0;
 };
 
 // ----------------------------------------------------------------------------- run context

@@ -44,7 +44,10 @@ extern "C" {
 
 typedef struct dac_handle dac_handle;
 
-enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1 };           /* compute/storage dtype */
+/* compute/storage dtype. DAC_FP8: bf16 activations, and every conv / linear whose input
+ * channels are a multiple of 64 runs on the block-scaled fp8 MFMA (OCP e4m3 weights and
+ * on-the-fly quantized activations, one E8M0 scale per 64-element block; BASELINE configs[4]). */
+enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1, DAC_FP8 = 2 };
 enum dac_src_dtype { DAC_SRC_F32 = 0, DAC_SRC_F16 = 1, DAC_SRC_BF16 = 2 };
 enum dac_mode { DAC_POSTERIOR = 0, DAC_SDE = 1 };       /* DenoisingModel.test(mode=) */
 enum dac_schedule { DAC_COSINE = 0, DAC_LINEAR = 1, DAC_CONSTANT = 2 };

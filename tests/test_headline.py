@@ -107,3 +107,22 @@ def test_headline_bf16_matches_reference(headline, unet_sd):
     ic, dc, out = restore("bf16", g, lq, n0, steps, unet_sd)
     check("headline_bf16", g, ic, dc, out, ctx_tol=2e-2, out_tol=8e-4)
     assert calculate_psnr(tensor2img(torch.from_numpy(out[0])), g["out_u8"]) > 50.0
+
+
+def test_headline_fp8_psnr(headline, unet_sd):
+    """fp8 handles (e4m3 MX GEMMs, BASELINE configs[4]) on the same fixture: the PSNR delta is
+    measured and bounded (measured: dPSNR 7.1e-4 dB, 30.7 dB against the reference's uint8
+    output, float max-rel 4.2e-3); the run must stay finite and batch-invariant."""
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    g, lq, n0, steps = headline
+    ic, dc, out = restore("fp8", g, lq, n0, steps, unet_sd)
+    for b in range(1, B):
+        assert np.array_equal(out[b], out[0]), b
+    assert np.isfinite(out).all()
+    u8 = tensor2img(torch.from_numpy(out[0]))
+    d_psnr = calculate_psnr(u8, g["lq_u8"]) - calculate_psnr(g["out_u8"], g["lq_u8"])
+    record("headline_fp8", delta_psnr_db=d_psnr, psnr_vs_ref_u8=calculate_psnr(u8, g["out_u8"]),
+           out_rel=rel(out[0], g["out"][0]), ctx_rel=max(rel(ic[0], g["image_context"][0]),
+                                                          rel(dc[0], g["degra_context"][0])))
+    assert abs(d_psnr) < 1e-2
+    assert rel(out[0], g["out"][0]) < 2e-2

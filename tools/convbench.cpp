@@ -9,6 +9,7 @@
 #include <cstring>
 #include <cmath>
 #include <vector>
+#include <algorithm>
 #include "../da-clip_amd/csrc/kernels.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
@@ -61,7 +62,146 @@ __global__ void ref_conv(ConvArgs a, int kh, int s, int p, int kws, float* out) 
   out[i] = acc;
 }
 
+// ---- fp8 (conv8.hip) check: host e4m3 quantization identical in spirit to engine.cpp.
+static uint8_t f2e4m3(float f) {
+  const uint8_t sign = std::signbit(f) ? 0x80 : 0;
+  const float a = std::fabs(f);
+  if (std::isnan(a)) return 0x7f;
+  if (a >= 464.f) return sign | 0x7e;
+  if (a < std::ldexp(1.f, -6)) { const int q = (int)std::nearbyint(a * 512.f); return sign | (uint8_t)(q >= 8 ? 8 : q); }
+  int e; std::frexp(a, &e);
+  int E = e - 1 + 7, q = (int)std::nearbyint((a / std::ldexp(1.f, e - 1) - 1.f) * 8.f);
+  if (q == 8) { q = 0; ++E; }
+  if (E > 15 || (E == 15 && q == 7)) return sign | 0x7e;
+  return sign | (uint8_t)(E << 3) | (uint8_t)q;
+}
+static float e4m3f(uint8_t b) {
+  const int s = b >> 7, E = (b >> 3) & 15, q = b & 7;
+  const float v = E ? std::ldexp(1.f + q / 8.f, E - 7) : std::ldexp(q / 8.f, -6);
+  return s ? -v : v;
+}
+static float bf2f(bf16 v) { return (float)v; }
+// Quantize rows of n values in 64-blocks: returns dequantized values (and e4m3 bytes + E8M0).
+static void quant_rows(const std::vector<float>& v, int rows, int n, int np, std::vector<float>& deq,
+                       std::vector<uint8_t>* q8, std::vector<uint8_t>* s8) {
+  deq.assign((size_t)rows * n, 0.f);
+  if (q8) { q8->assign((size_t)rows * np, 0); s8->assign((size_t)rows * (np / 64), 127); }
+  for (int r = 0; r < rows; ++r)
+    for (int b = 0; b * 64 < n; ++b) {
+      float mx = 0.f;
+      for (int k = 64 * b; k < std::min(n, 64 * b + 64); ++k) mx = std::max(mx, std::fabs(v[(size_t)r * n + k]));
+      int e = mx > 0.f ? (int)std::ceil(std::log2(mx / 448.f)) : 0;
+      e = std::min(126, std::max(-126, e));
+      if (s8) (*s8)[(size_t)r * (np / 64) + b] = (uint8_t)(127 + e);
+      for (int k = 64 * b; k < std::min(n, 64 * b + 64); ++k) {
+        const uint8_t q = f2e4m3(v[(size_t)r * n + k] * std::ldexp(1.f, -e));
+        if (q8) (*q8)[(size_t)r * np + k] = q;
+        deq[(size_t)r * n + k] = e4m3f(q) * std::ldexp(1.f, e);
+      }
+    }
+}
+// Host direct conv (NHWC x [B][H][W][Cin], w [Cout][kh][kw][Cin]) for the fp8 check.
+static void host_conv(const std::vector<float>& x, const std::vector<float>& w, int B, int H, int W, int Cin,
+                      int Cout, int k, int s, int p, std::vector<float>& y, int& Ho, int& Wo) {
+  Ho = (H + 2 * p - k) / s + 1; Wo = (W + 2 * p - k) / s + 1;
+  y.assign((size_t)B * Ho * Wo * Cout, 0.f);
+  for (int b = 0; b < B; ++b)
+    for (int oh = 0; oh < Ho; ++oh)
+      for (int ow = 0; ow < Wo; ++ow)
+        for (int n = 0; n < Cout; ++n) {
+          double acc = 0;
+          for (int kh = 0; kh < k; ++kh)
+            for (int kw = 0; kw < k; ++kw) {
+              const int ih = oh * s - p + kh, iw = ow * s - p + kw;
+              if (ih < 0 || iw < 0 || ih >= H || iw >= W) continue;
+              const float* xp = &x[(((size_t)b * H + ih) * W + iw) * Cin];
+              const float* wp = &w[(((size_t)n * k + kh) * k + kw) * Cin];
+              for (int c = 0; c < Cin; ++c) acc += (double)xp[c] * wp[c];
+            }
+          y[(((size_t)b * Ho + oh) * Wo + ow) * Cout + n] = (float)acc;
+        }
+}
+static int fp8_check() {
+  struct S8 { const char* name; int B, H, W, cin, cout, k, s, p; };
+  const S8 shapes[] = {{"3x3 128->128 16x16", 2, 16, 16, 128, 128, 3, 1, 1},
+                       {"3x3 64->64 16x16", 2, 16, 16, 64, 64, 3, 1, 1},
+                       {"1x1 256->384 8x8", 2, 8, 8, 256, 384, 1, 1, 0},
+                       {"4x4s2 64->128 16x16", 2, 16, 16, 64, 128, 4, 2, 1}};
+  int fails = 0;
+  for (const S8& sh : shapes) {
+    const size_t nx = (size_t)sh.B * sh.H * sh.W * sh.cin;
+    const int K = sh.k * sh.k * sh.cin, Kp = (K + 127) / 128 * 128;
+    std::vector<float> xf(nx), wf((size_t)sh.cout * K);
+    uint32_t h = 12345;
+    auto rnd = [&]() { h = h * 1664525u + 1013904223u; return ((h >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb(nx);
+    for (size_t i = 0; i < nx; ++i) { xb[i] = (bf16)(rnd() * 4.f * (1 + (i % 7))); xf[i] = bf2f(xb[i]); }
+    for (auto& v : wf) v = rnd() * 0.2f;
+    if (getenv("FP8_ONEHOT")) {         // y[m][n] = (n == m % 128): reveals a permutation
+      for (size_t i = 0; i < nx; ++i) { const size_t m = i / sh.cin, c = i % sh.cin; xf[i] = c == m % 128 ? 1.f : 0.f; xb[i] = (bf16)xf[i]; }
+      for (size_t i = 0; i < wf.size(); ++i) wf[i] = (i % K) == (i / K) % sh.cin ? 1.f : 0.f;
+    }
+    std::vector<float> xd, wd;
+    std::vector<uint8_t> w8, s8;
+    quant_rows(xf, (int)(nx / sh.cin), sh.cin, sh.cin, xd, nullptr, nullptr);   // per pixel, 64-ch blocks
+    quant_rows(wf, sh.cout, K, Kp, wd, &w8, &s8);
+    int Ho, Wo;
+    std::vector<float> yq, yf;
+    host_conv(xd, wd, sh.B, sh.H, sh.W, sh.cin, sh.cout, sh.k, sh.s, sh.p, yq, Ho, Wo);
+    host_conv(xf, wf, sh.B, sh.H, sh.W, sh.cin, sh.cout, sh.k, sh.s, sh.p, yf, Ho, Wo);
+    void *dx, *dy, *dz; uint8_t *dw, *ds;
+    CK(hipMalloc(&dx, nx * 2)); CK(hipMalloc(&dy, yq.size() * 2)); CK(hipMalloc(&dz, 256));
+    CK(hipMalloc(&dw, w8.size())); CK(hipMalloc(&ds, s8.size()));
+    CK(hipMemset(dz, 0, 256));
+    CK(hipMemcpy(dx, xb.data(), nx * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, w8.data(), w8.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(ds, s8.data(), s8.size(), hipMemcpyHostToDevice));
+    ConvArgs a{};
+    a.x1 = dx; a.ld1 = sh.cin; a.C1 = sh.cin; a.Cin = sh.cin; a.Hs = sh.H; a.Ws = sh.W; a.B = sh.B;
+    a.Ho = Ho; a.Wo = Wo; a.Cout = sh.cout; a.K = K; a.y = dy; a.ldy = sh.cout; a.zero = dz;
+    if (!conv8_ok(a, sh.k, sh.k, sh.s, sh.p)) { printf("fp8 %-22s not eligible\n", sh.name); ++fails; continue; }
+    conv8(a, sh.k, sh.k, sh.s, sh.p, dw, ds, Kp, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<bf16> yb(yq.size());
+    CK(hipMemcpy(yb.data(), dy, yb.size() * 2, hipMemcpyDeviceToHost));
+    double mq = 0, mf = 0, ref = 0;
+    int nnan = 0, shown = 0;
+    for (size_t i = 0; i < yq.size(); ++i) {
+      const float g = bf2f(yb[i]);
+      if (!std::isfinite(g)) ++nnan;
+      if (shown < 6 && (!std::isfinite(g) || std::fabs(g - yq[i]) > 0.05 * std::fabs(yq[i]) + 0.5)) {
+        printf("   m=%zu n=%zu got %g want %g\n", i / sh.cout, i % sh.cout, g, yq[i]);
+        ++shown;
+      }
+      mq = std::max(mq, std::fabs((double)bf2f(yb[i]) - yq[i]));
+      mf = std::max(mf, std::fabs((double)bf2f(yb[i]) - yf[i]));
+      ref = std::max(ref, std::fabs((double)yf[i]));
+    }
+    if (getenv("FP8_DUMP")) {
+      FILE* f = fopen(getenv("FP8_DUMP"), "a");
+      fprintf(f, "%s\n", sh.name);
+      for (size_t i = 0; i < yq.size(); ++i)
+        if (bf2f(yb[i]) != 0.f) fprintf(f, "%zu %zu %g\n", i / sh.cout, i % sh.cout, bf2f(yb[i]));
+      fclose(f);
+    }
+    if (getenv("FP8_ONEHOT"))
+      for (int m = 0; m < 20; ++m) {
+        printf("   m=%d nonzero n:", m);
+        for (int n = 0; n < std::min(sh.cout, 256); ++n) if (bf2f(yb[(size_t)m * sh.cout + n]) != 0.f) printf(" %d(%g)", n, bf2f(yb[(size_t)m * sh.cout + n]));
+        printf("\n");
+      }
+    if (nnan) printf("   %d non-finite outputs\n", nnan);
+    const bool ok = mq / ref < 1e-2 && nnan == 0;
+    printf("fp8 %-22s vs quantized-operand ref %.2e (%s), vs exact operands %.2e\n", sh.name, mq / ref,
+           ok ? "OK" : "FAIL", mf / ref);
+    fails += !ok;
+    CK(hipFree(dx)); CK(hipFree(dy)); CK(hipFree(dz)); CK(hipFree(dw)); CK(hipFree(ds));
+  }
+  return fails;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
   int iters = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 && argv[2][0] ? argv[2] : nullptr;   // substring filter
   const bool check = argc > 3 && !strcmp(argv[3], "check");
