@@ -1184,6 +1184,10 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     }
   }
   if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
+    if (conv7_ok(a)) {
+      conv7(a, st);
+      return;
+    }
     if (a.Cin == 8 && a.K == (a.cwrap ? 2 : 1) * 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {
       const int Mg = a.B * a.Ho * a.Wo;
       dim3 g((Mg + 255) / 256, (a.Cout + 63) / 64, 1);
