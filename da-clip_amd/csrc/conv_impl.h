@@ -1167,6 +1167,12 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   // (init conv Cin=8, patch embed, final conv Cout=3, LinearAttention to_out amode=1).
   constexpr bool V2 = (KH == 1 || KH == 3 || KH == 4);
   const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2) {
+    if (g_conv3_force < 0 && conv3n_ok(a)) {   // final_conv: conv_edge.hip
+      conv3n(a, st);
+      return;
+    }
+  }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     // Narrow output (the final conv, Cout = 3): v4 row-halo tiles with 16 output channels and
     // the general (scalar-capable) epilogue; the A operand dominates, and v4 reads each input

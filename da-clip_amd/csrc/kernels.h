@@ -58,9 +58,13 @@ inline bool conv3w_ok(const ConvArgs& a) {
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
 // init_conv (7x7, Cin 8 row-tap layout, Cout 64, bf16, plain or split-precision weights):
-// weight-stationary persistent kernel (conv7.hip).
+// weight-stationary persistent kernel (conv_edge.hip).
 bool conv7_ok(const ConvArgs& a);
 void conv7(const ConvArgs& a, hipStream_t st);
+// final_conv (3x3, Cin 64 -> Cout <= 4, bf16, plain or split-precision weights, Wo % 64 == 0):
+// streaming kernel with hi/lo as separate MFMA rows (conv_edge.hip).
+bool conv3n_ok(const ConvArgs& a);
+void conv3n(const ConvArgs& a, hipStream_t st);
 int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 
 // fp8 (e4m3, MX block scales) implicit GEMM for bf16 activations (conv8.hip): w8 [Cout][Kp]
