@@ -13,8 +13,12 @@
 // L = 50 (B/32) tokens, 12 heads x 64; tiny, one workgroup per (image, head), fp32 math.
 #include "common.h"
 #include "kernels.h"
+#include <cstdlib>
 
 namespace dac {
+
+// 1: always the staged-tile kernel (DAC_FLASH_OLD=1, or dac_op_attention variant 1).
+int g_flash_old = getenv("DAC_FLASH_OLD") ? atoi(getenv("DAC_FLASH_OLD")) : 0;
 
 template <typename T, int QG>
 __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qkv, T* o, int L,
@@ -132,8 +136,8 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
             tmax = fmaxf(tmax, s[mi][r]);
           }
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      tmax = red16_max(tmax);
+      tmax = red32_max(tmax);
       const float mnew = fmaxf(mrun[g], tmax * c);
       const float corr = sizeof(T) == 2 ? __builtin_amdgcn_exp2f(mrun[g] - mnew) : exp2f(mrun[g] - mnew);
       float psum = 0.f;
@@ -146,8 +150,8 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
           s[mi][r] = p;
           psum += p;
         }
-      psum += __shfl_xor(psum, 16, 64);
-      psum += __shfl_xor(psum, 32, 64);
+      psum = red16_sum(psum);
+      psum = red32_sum(psum);
       lrun[g] = lrun[g] * corr + psum;
       mrun[g] = mnew;
 #pragma unroll
@@ -198,8 +202,214 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
   }
 }
 
+// ------------------------------------------------------------------ K/V-resident variant
+// flash_kv_kernel (bf16, L % 128 == 0, L <= 1024 — the UNet's 32x32 SpatialTransformer levels
+// at 256^2): a block owns QG*128 queries of one (image, head) with 8 waves and keeps the head's
+// WHOLE K and V in LDS (L x 64 B each, 128 KB at L = 1024):
+//  * every K/V byte is DMA'd (global_load_lds, issued all at once in the prologue, 128-key
+//    chunks in order) straight into LDS in its natural [key][d] layout, 16-byte chunk XOR-
+//    swizzled by ((key >> 2) & 1) * 2 at the source (conflict-free for both reads below);
+//    the only barriers are one per chunk as it lands, never a write-after-read;
+//  * S^T = K Q^T: A = K rows (ds_read_b128), B = the wave's 16 queries (registers);
+//  * O^T += V^T P^T: A = V^T read with ds_read_b64_tr_b16 (hardware transpose of the [key][d]
+//    image), in exactly the key order the S^T accumulators hold P in (keys 4g..4g+3 and
+//    16+4g..16+4g+3 of a 32-key step), so P feeds the MFMA straight from registers;
+//  * each K / V fragment read serves all QG query groups of the wave; online softmax in the
+//    log2 domain, the row sums kept per lane and reduced across lanes once at the end.
+constexpr int FKV_NW = 8;
+#ifndef DAC_FKV_SKIP
+#define DAC_FKV_SKIP 1
+#endif
+DEV int fkv_swz(int key) { return ((key >> 2) & 1) << 1; }
+template <int N> DEV void fkv_wait(int n) {
+  // s_waitcnt vmcnt(n) for a runtime n in [0, N] (the immediate must be a constant).
+  if constexpr (N > 0) {
+    if (n >= N) { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); return; }
+    fkv_wait<N - 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+template <int QG>
+__global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __restrict__ qkv, bf16* o, int L,
+                                                              int H, float scale) {
+  constexpr int D = 32;
+  extern __shared__ __attribute__((aligned(1024))) char fkv_smem[];
+  char* sK = fkv_smem;
+  char* sV = fkv_smem + (size_t)L * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xq = n / 8, xr = n % 8, xcd = id % 8;
+  const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + id / 8;
+  const int bx = t % gx, h = (t / gx) % gy, b = t / (gx * gy);
+  const int ld = 3 * H * D;
+  const bf16* base = qkv + (size_t)b * L * ld;
+
+  // Q fragments first (their loads retire before the K/V DMAs in vmcnt order).
+  u32x4 qf[QG];
+  int qi[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    qi[g] = bx * (FKV_NW * 16 * QG) + wave * (16 * QG) + g * 16 + lr;
+    qf[g] = *reinterpret_cast<const u32x4*>(base + (size_t)qi[g] * ld + h * D + lg * 8);
+  }
+  // K / V DMA: instruction n fills keys 16n..16n+15 (1 KB); chunk c = instructions 8c..8c+7,
+  // wave w issues instruction 8c + w of K and of V (2 per wave per chunk).
+  const int NC = L >> 7;
+  {
+    const int kl = lane >> 2, ch = lane & 3;
+    for (int c = 0; c < NC; ++c) {
+      const int nn = 8 * c + wave;
+      const int key = 16 * nn + kl;
+      const bf16* src = base + (size_t)key * ld + h * D + 8 * (ch ^ fkv_swz(key));
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + H * D),
+                                       (__attribute__((address_space(3))) void*)(sK + nn * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * H * D),
+                                       (__attribute__((address_space(3))) void*)(sV + nn * 1024), 16, 0, 0);
+    }
+  }
+
+  f32x4 oacc[QG][2];
+  float mrun[QG], lpart[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    oacc[g][0] = oacc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mrun[g] = -INFINITY;
+    lpart[g] = 0.f;
+  }
+  const float cs = scale * 1.4426950408889634f;
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+  for (int c = 0; c < NC; ++c) {
+    fkv_wait<14>(2 * (NC - 1 - c));             // this wave's DMAs of chunk c have landed
+    __builtin_amdgcn_s_barrier();                // ... and every other wave's
+    asm volatile("" ::: "memory");
+    const int kb = c * 128;
+    u32x4 kf[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int key = kb + mi * 16 + lr;
+      kf[mi] = *reinterpret_cast<const u32x4*>(sK + key * 64 + ((lg ^ fkv_swz(key)) << 4));
+    }
+    // V^T fragments: step st (32 keys), d tile dm: rows = keys, lane (4q+p) addresses key
+    // kb + 32st + 4lg + q (+16), columns dm*16 + 4p .. +3.
+    u32x4 vf[4][2];
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int dm = 0; dm < 2; ++dm) {
+        uint32_t w[4];
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+          const int key = kb + 32 * st + 16 * hi + 4 * lg + (lr >> 2);
+          const int byte = (dm * 16 + 4 * (lr & 3)) * 2;          // 8-byte column group
+          const int off = key * 64 + ((((byte >> 4) ^ fkv_swz(key)) << 4) | (byte & 15));
+          const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(sV + off));
+          const uint2 u = __builtin_bit_cast(uint2, r);
+          w[2 * hi] = u.x;
+          w[2 * hi + 1] = u.y;
+        }
+        vf[st][dm] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      f32x4 s[8];
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        s[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Mma<bf16>::run(s[mi], kf[mi], qf[g]);
+      }
+      float tmax = s[0][0];
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[mi][r]);
+      tmax = red16_max(tmax);
+      tmax = red32_max(tmax);
+      const float mnew = fmaxf(mrun[g], tmax * cs);
+      float psum = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
+          s[mi][r] = p;
+          psum += p;
+        }
+      // Rescale only when some query's running max moved (exact: otherwise corr == 1).
+      if (DAC_FKV_SKIP == 0 || __any(mnew != mrun[g])) {
+        const float corr = __builtin_amdgcn_exp2f(mrun[g] - mnew);
+        lpart[g] *= corr;
+#pragma unroll
+        for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+      }
+      lpart[g] += psum;                          // this lane's keys only; reduced at the end
+      mrun[g] = mnew;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        bf16x8 pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (bf16)s[2 * st][j];
+          pb[4 + j] = (bf16)s[2 * st + 1][j];
+        }
+        const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
+#pragma unroll
+        for (int dm = 0; dm < 2; ++dm) Mma<bf16>::run(oacc[g][dm], vf[st][dm], pbu);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    float l = lpart[g];
+    l = red16_sum(l);
+    l = red32_sum(l);
+    const float inv = 1.f / l;
+    bf16* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
+#pragma unroll
+    for (int dm = 0; dm < 2; ++dm) {
+      bf16x2_t v0, v1;
+      v0[0] = (bf16)(oacc[g][dm][0] * inv); v0[1] = (bf16)(oacc[g][dm][1] * inv);
+      v1[0] = (bf16)(oacc[g][dm][2] * inv); v1[1] = (bf16)(oacc[g][dm][3] * inv);
+      uint2 st;
+      st.x = __builtin_bit_cast(uint32_t, v0);
+      st.y = __builtin_bit_cast(uint32_t, v1);
+      *reinterpret_cast<uint2*>(out + dm * 16 + 4 * lg) = st;
+    }
+  }
+}
+
 template <typename T>
 void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (L % 128 == 0 && L <= 1024 && !g_flash_old) {
+      // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
+      // fills the chip, else 2 (or 1).
+      const size_t smem = (size_t)L * 128;
+      static bool attr = false;
+      if (!attr) {                               // > 64 KB of dynamic LDS must be opted into
+        attr = true;
+        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+      }
+      if (L % 512 == 0 && (long)(L / 512) * H * B >= 256) {
+        dim3 g(L / 512, H, B);
+        flash_kv_kernel<4><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+      } else if (L % 256 == 0) {
+        dim3 g(L / 256, H, B);
+        flash_kv_kernel<2><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+      } else {
+        dim3 g(L / 128, H, B);
+        flash_kv_kernel<1><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+      }
+      return;
+    }
+  }
   // Two 16-query groups per wave (128 queries per block) once that still leaves >= 2 blocks
   // per CU: each staged K/V tile and its two barriers then serve twice the queries.
   if ((long)((L + 127) / 128) * H * B >= 512) {

@@ -278,6 +278,20 @@ double dac_encode_flops(dac_handle* h, int B) {
   return f;
 }
 
+int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype, int variant,
+                     void* stream) {
+  if (!qkv || !out || B <= 0 || L <= 0 || H <= 0 || (dtype != DAC_F32 && dtype != DAC_BF16) ||
+      variant < 0 || variant > 1)
+    return DAC_E_ARG;
+  const int keep = dac::g_flash_old;
+  dac::g_flash_old = variant == 1 ? 1 : keep;
+  const float scale = 1.f / std::sqrt(32.f);
+  if (dtype == DAC_BF16) dac::flash_attn_d32<__bf16>(qkv, out, B, L, H, scale, (hipStream_t)stream);
+  else dac::flash_attn_d32<float>(qkv, out, B, L, H, scale, (hipStream_t)stream);
+  dac::g_flash_old = keep;
+  return hipGetLastError() == hipSuccess ? DAC_OK : DAC_E_HIP;
+}
+
 int dac_profile_enable(dac_handle* h, int kernel_id) {
   return guard(h, [&]() -> int {
     h->eng->prof.kernel_id = kernel_id;

@@ -93,6 +93,19 @@ DEV float gelu_fast(float x) {
   return 0.5f * x * (x >= 0.f ? 2.f - q : q);
 }
 
+// Cross-row reductions on the VALU (gfx950 v_permlane16/32_swap): swapping a register pair
+// that both hold x leaves {x, partner} in the pair (in some order), so combining the two gives
+// x (op) x^16 or x (op) x^32 in every lane -- the same values as __shfl_xor, without an
+// LDS-crossbar round trip and its lgkmcnt wait. Inline asm: the compiler folds the builtin's
+// two results into one when both inputs are the same value (it then combined x with itself);
+// the s_nop 1 covers the VALU-write -> permlane-read hazard the asm hides from the compiler.
+DEV void perm16_swap(float& a, float& b) { asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+DEV void perm32_swap(float& a, float& b) { asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
+DEV float red16_sum(float v) { float a = v, b = v; perm16_swap(a, b); return a + b; }
+DEV float red32_sum(float v) { float a = v, b = v; perm32_swap(a, b); return a + b; }
+DEV float red16_max(float v) { float a = v, b = v; perm16_swap(a, b); return fmaxf(a, b); }
+DEV float red32_max(float v) { float a = v, b = v; perm32_swap(a, b); return fmaxf(a, b); }
+
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -81,6 +81,11 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   return a.Cout <= 64 ? 1 : 2;
 }
 
+bool conv_res_fusable(const ConvArgs& a) {
+  return a.w2 && a.y2 && a.ldy2 % 8 == 0 && a.bias2 == nullptr && conv_variant(a, 3, 2) == 12 &&
+         a.Cout % 64 == 0;
+}
+
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {
   if (kh == 3 && kw == 3 && s == 1 && p == 1) conv_dispatch<T, 3, 3, 1, 1>(a, st);

@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
       // lane (lr, g) holds rows 4g..4g+3 of pixel lr: g = 0 the hi rows, g = 1 the lo rows.
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = NP == 2 ? acc[q][e] + __shfl_xor(acc[q][e], 16, 64) : acc[q][e];
+      for (int e = 0; e < 4; ++e) v[e] = NP == 2 ? red16_sum(acc[q][e]) : acc[q][e];
       // Lane (lr, g) stores channel g of pixel lr (one 2-byte store instruction per wave and
       // row; with ldy >= 4 the padding channels Cout..3 are written as 0).
       float mine = 0.f;

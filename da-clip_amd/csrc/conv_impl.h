@@ -13,6 +13,7 @@
 // XOR-swizzled by (row>>1)&7 so the 16 rows read by a ds_read_b128 lane group hit distinct
 // banks.
 #pragma once
+#include <cstdlib>
 #include <type_traits>
 #include "common.h"
 #include "kernels.h"
@@ -246,14 +247,14 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
       float sm = 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) sm += v[e];
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
+      sm = red16_sum(sm);
+      sm = red32_sum(sm);
       const float mean = sm * (1.f / 64.f);
       float q = 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) { const float d = v[e] - mean; q += d * d; }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
+      q = red16_sum(q);
+      q = red32_sum(q);
       const float rstd = 1.f / sqrtf(q * (1.f / 64.f) + a.ln_eps);
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = (v[e] - mean) * rstd * gl[e];
@@ -751,9 +752,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   constexpr int AROWS = NA_MAX * RPI;
   constexpr int NB = 3 * BN / RPI;                           // B DMA instructions per stage
   constexpr int BGX = (NB + NW - 1) / NW, BGN = NB / NW;     // per wave (max / min)
-  constexpr int STAGE = (AROWS + 3 * BN) * CK;
+  // FL bit 4: fused 1x1 second output (ConvArgs::w2 / y2): the centre-tap A fragments of the
+  // kh = 1 stages also multiply the w2 rows (hi and lo parts), staged after the 3*BN weight
+  // rows, into a second accumulator set written by a plain register epilogue.
+  constexpr bool RES = (FL & 16) != 0;
+  constexpr int RROWS = RES ? 2 * BN : 0;
+  constexpr int STAGE = (AROWS + 3 * BN + RROWS) * CK;
   static_assert(SLOTS == 8 || SLOTS == 4, "CK");
   static_assert((3 * BN) % RPI == 0 && KSTEPS >= 1 && TM >= 1 && TN >= 1, "tile");
+  static_assert(!RES || (ST == 2 && (FL & 8) && BN % RPI == 0), "fused res: swapped tiles, 2 stages");
   static_assert(STAGE % 256 == 0 && (AROWS * CK) % 256 == 0, "bank-line aligned regions");
   static_assert(ST == 2 || ST == 3 || ST == 4, "stages");
   constexpr int VMW = (ST - 2) * (AGN + BGN);
@@ -816,6 +823,25 @@ conv3i_kernel(ConvArgs a, int RW) {
     b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
                           : nullptr;
   }
+  // Res-weight DMA: instruction j of this wave fills rows 3*BN + (wave + j*NW)*RPI + lane/SLOTS
+  // (part = local row / BN: 0 hi, 1 lo).
+  constexpr int RGX = RES ? (RROWS / RPI + NW - 1) / NW : 1;
+  const T* r_ptr[RGX];
+  int r_ls[RGX];
+  const int nparts = RES && a.w2_dual ? 2 : 1;
+  if constexpr (RES) {
+#pragma unroll
+    for (int j = 0; j < RGX; ++j) {
+      const int lrow = (wave + j * NW) * RPI + lane / SLOTS;
+      const int row = 3 * BN + lrow;
+      r_ls[j] = SB::slot(row, lane % SLOTS) * VE;
+      const int part = lrow / BN;
+      const int n = n0 + wperm64(lrow % BN);
+      r_ptr[j] = (lrow < RROWS && part < nparts && n < a.Cout)
+                     ? reinterpret_cast<const T*>(a.w2) + (size_t)n * a.Cin * nparts + part * a.Cin
+                     : nullptr;
+    }
+  }
   // Fragment offsets (stage-relative bytes).
   const int lr = lane & 15, lg = lane >> 4;
   int aoff[NF][KSTEPS], boff[3][TN][KSTEPS];
@@ -866,9 +892,26 @@ conv3i_kernel(ConvArgs a, int RW) {
                                          16, 0, 0);
       }
     }
+    if constexpr (RES && kh == 1) {
+#pragma unroll
+      for (int j = 0; j < RGX; ++j) {
+        if ((wave + j * NW) * RPI < RROWS) {                        // wave-uniform
+          const char* src = r_ptr[j] ? reinterpret_cast<const char*>(r_ptr[j] + ci0 + r_ls[j]) : zero;
+          __builtin_amdgcn_global_load_lds(
+              (gbl_void_t*)src, (lds_void_t*)(st + (AROWS + 3 * BN) * CK + (wave + j * NW) * RPI * CK), 16, 0, 0);
+        }
+      }
+    }
   };
 
   f32x4 acc[TM][TN];
+  f32x4 accR[RES ? TM : 1][RES ? TN : 1];
+  if constexpr (RES) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) accR[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -876,13 +919,29 @@ conv3i_kernel(ConvArgs a, int RW) {
   EpiTerms<SWAP ? 1 : TN> et;
   if constexpr (!SWAP) et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
 
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, auto khc) {
+    constexpr int kh = decltype(khc)::value;
     const char* st = smem + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       u32x4 fa[NF];
 #pragma unroll
       for (int s = 0; s < NF; ++s) fa[s] = *reinterpret_cast<const u32x4*>(st + aoff[s][ks]);
+      if constexpr (RES && kh == 1) {
+        // Fused res_conv: centre tap (kw = 1) fragments F_{i+1} times the w2 rows.
+        for (int pt = 0; pt < nparts; ++pt) {
+          u32x4 fr[TN];
+#pragma unroll
+          for (int jn = 0; jn < TN; ++jn) {
+            const int row = 3 * BN + pt * BN + wn * WTN + jn * 16 + lr;
+            fr[jn] = *reinterpret_cast<const u32x4*>(st + AROWS * CK + row * CK + (SB::slot(row, ks * 4 + lg) << 4));
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jn = 0; jn < TN; ++jn) Mma<T>::run(accR[i][jn], fr[jn], fa[i + 1]);
+        }
+      }
       if constexpr (FL & 2) {
         u32x4 fb[3][TN];
 #pragma unroll
@@ -936,7 +995,7 @@ conv3i_kernel(ConvArgs a, int RW) {
     asm volatile("" ::: "memory");
     if (s + ST - 1 < S) issue(c + CN, std::integral_constant<int, KN>{}, nbuf);
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
-    compute(buf);
+    compute(buf, khc);
     buf = buf + 1 == ST ? 0 : buf + 1;
     nbuf = nbuf + 1 == ST ? 0 : nbuf + 1;
   };
@@ -957,6 +1016,19 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
     epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); });
+    if constexpr (RES) {
+      // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
+      bf16* y2 = reinterpret_cast<bf16*>(a.y2);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const size_t m = (size_t)rm(wm * WTM + TM * lr + i);
+        float v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = accR[i][e >> 2][e & 3] + (a.bias2 ? a.bias2[nb + e] : 0.f);
+        store_vec<bf16>(y2 + m * a.ldy2 + nb, v);
+        store_vec<bf16>(y2 + m * a.ldy2 + nb + 8, v + 8);
+      }
+    }
   } else {
     conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK, TM>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
   }
@@ -1158,6 +1230,8 @@ inline int conv3w_blocks(int ntiles) {
 
 template <typename T, int KH, int KW, int S, int P>
 void conv_dispatch(const ConvArgs& a, hipStream_t st) {
+  // A fused second output is only requested after conv_res_fusable(a) said the v4 path takes it.
+  if (a.y2 && !(KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2 && conv_res_fusable(a))) abort();
   const int M = a.B * a.Ho * a.Wo;
   const bool batched = a.w_bstride > 0;
   const int Mg = batched ? a.Ho * a.Wo : M;
@@ -1215,8 +1289,13 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         // v3 at every 3x3 shape of the UNet whose row width is a multiple of 64).
         // bf16 with whole 64-channel tiles: swapped operands + register epilogue (FL bit 3),
         // 4-9 % faster than the LDS-staged epilogue at every v4 shape of the UNet.
-        if constexpr (sizeof(T) == 2)
-          if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) return;
+        if constexpr (sizeof(T) == 2) {
+          if (a.y2) {
+            if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
+          } else if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) {
+            return;
+          }
+        }
         if (conv3i_try<T, 256, 64, 4, 1, 64, 2, 4>(a, st)) return;
         // Rows of 32 (the 32x32 level), Cout <= 256: 128x64 tiles of 32-pixel wave tiles
         // (TM = 2), 8 % faster than v3 in the UNet; the 512-wide convs stay on v3 (v4 with

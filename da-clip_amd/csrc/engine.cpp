@@ -47,6 +47,11 @@ static int key_role(const std::string& k) {
 }
 template <typename T>
 static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
+// DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
+static bool no_res_fuse() {
+  static const int v = getenv("DAC_NO_RES_FUSE") ? atoi(getenv("DAC_NO_RES_FUSE")) : 0;
+  return v != 0;
+}
 // DAC_EMU_WSKIP: comma-separated key substrings whose weights stay fp32 under DAC_EMU_W.
 static bool emu_w_key(const std::string& k) {
   if (!(emu_w() & key_role(k))) return false;
@@ -366,10 +371,18 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
   const double M = (double)B * a.Ho * a.Wo;
-  const double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
-  r.flops += fl;
+  double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   Profiler* p = r.prof;
   const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
+  bool fused = false;
+  if (e.fuse1x1) {
+    a.w2 = e.fuse1x1->w; a.w2_dual = e.fuse1x1->dual; a.bias2 = e.fuse1x1->b; a.y2 = e.y2; a.ldy2 = e.ldy2;
+    fused = sizeof(T) == 2 && !use8 && a.w2 && cw.kh == 3 && stride == 1 && pad == 1 && !up &&
+            e.fuse1x1->cout == cw.cout && e.fuse1x1->cin == cw.cin && conv_res_fusable(a);
+    if (!fused) { a.w2 = nullptr; a.bias2 = nullptr; a.y2 = nullptr; a.w2_dual = 0; a.ldy2 = 0; }
+    else fl += 2.0 * M * cw.cout * e.fuse1x1->cin_real;
+  }
+  r.flops += fl;
   const int cls = cw.kh * 100 + (use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
   const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == cls);
   if (r.dry) {
@@ -386,6 +399,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   if (use8) conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
   else conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
   emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
+  if (fused) emu_round<T>(r, e.y2, e.ldy2, (size_t)M, cw.cout);
   if (timed) {
     HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
     p->used++;
@@ -393,17 +407,19 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     p->flops += fl;
     if (p->kernel_id == Profiler::ALL) {
       char lab[160];
-      snprintf(lab, sizeof lab, "c%d %3dx%-3d%s s%d %4d->%-4d%s%s%s%s", cls, Hs, Ws, up ? "^" : " ",
+      snprintf(lab, sizeof lab, "c%d %3dx%-3d%s s%d %4d->%-4d%s%s%s%s%s", cls, Hs, Ws, up ? "^" : " ",
                stride, cw.cin_real, cw.cout, e.res1 ? " +r" : "", e.res2 ? " +r2" : "",
-               e.ss ? " ss" : "", e.w_bstride ? " perimg" : "");
+               e.ss ? " ss" : "", e.w_bstride ? " perimg" : "", fused ? " +1x1" : "");
       p->labels.push_back(lab);
       p->lflops.push_back(fl);
     }
     // Algorithmic HBM bytes: every operand touched once (input, weights, output, residuals).
     const double es = sizeof(T);
     p->bytes += es * ((double)B * Hs * Ws * cw.cin_real + (double)cw.cout * cw.kh * cw.kw * cw.cin +
-                      M * cw.cout * (1 + (e.res1 ? 1 : 0) + (e.res2 ? 1 : 0)));
+                      M * cw.cout * (1 + (e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0)));
   }
+  if (e.fuse1x1 && !fused)
+    conv_call<T>(r, *e.fuse1x1, x1, ld1, C1, x2, ld2, B, Hs, Ws, 0, 1, 0, e.y2, e.ldy2, Epi());
 }
 
 template <typename T>
@@ -706,12 +722,17 @@ struct UNetNet {
     T* h1 = r.alloc<T>(M * rb.dout);
     Epi e1;
     e1.ss = ss + rb.ss_off; e1.ss_ld = ss_total; e1.act = ACT_SILU;
-    conv_call<T>(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h1, rb.dout, e1);
     const void* res = xa;
     int ldr = Ca;
+    T* rr = rb.has_res ? r.alloc<T>(M * rb.dout) : nullptr;
+    if (rb.has_res && !no_res_fuse()) {
+      // res_conv rides along in block1's conv kernel (same input; conv_call falls back to a
+      // separate launch when the kernel cannot take it).
+      e1.fuse1x1 = &rb.res; e1.y2 = rr; e1.ldy2 = rb.dout;
+    }
+    conv_call<T>(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h1, rb.dout, e1);
     if (rb.has_res) {
-      T* rr = r.alloc<T>(M * rb.dout);
-      conv_call<T>(r, rb.res, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 0, rr, rb.dout, Epi());
+      if (no_res_fuse()) conv_call<T>(r, rb.res, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 0, rr, rb.dout, Epi());
       res = rr;
       ldr = rb.dout;
     }

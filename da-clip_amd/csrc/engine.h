@@ -121,6 +121,11 @@ struct Epi {
   long long w_bstride = 0;       // per-image weights (ConvArgs::w_bstride)
   const float* ln_g = nullptr;   // row LayerNorm over Cout in the epilogue (ConvArgs::ln_g)
   float ln_eps = 1e-5f;
+  // 3x3 convs: a 1x1 conv over the same input written to y2 (the ResBlock res_conv), fused
+  // into the conv kernel when the dispatcher can (ConvArgs::w2), else run right after it.
+  const ConvW* fuse1x1 = nullptr;
+  void* y2 = nullptr;
+  int ldy2 = 0;
 };
 
 template <typename T>

@@ -46,7 +46,16 @@ struct ConvArgs {
   // channel ci - cwrap (two-source layers; then split by C1 as usual); for the 7x7 row-tap
   // layout, kernel row kt >= KH reads row kt - KH.
   int cwrap;
+  // Fused second output (the ResBlock's 1x1 res_conv, module_util.py:142,153), 3x3 v4 kernels
+  // only: y2[m, n] = sum_c x[m @ centre tap, c] * w2[n, c] (+ bias2), over the same (x1 | x2)
+  // input the conv reads; w2 is [Cout][Cin] bf16, or [Cout][hi Cin | lo Cin] with w2_dual.
+  const void* w2;
+  const float* bias2;
+  int w2_dual;
+  void* y2; int ldy2;
 };
+// The dispatcher can fuse a_w2/y2 into this 3x3 conv (bf16 v4 256x64 swapped-operand tiles).
+bool conv_res_fusable(const ConvArgs& a);
 
 // Shapes served by the weight-stationary 3x3 kernel (conv_impl.h conv3w_kernel, bf16 only).
 inline bool conv3w_ok(const ConvArgs& a) {
@@ -89,6 +98,7 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
 // SpatialTransformer, attention.py:170-193) -> o [B*L, H*D].
 template <typename T>
 void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st);
+extern int g_flash_old;
 
 // CLIP text tower helpers: token + positional embedding gather (ids outside [0, V) -> NaN),
 // EOT-row gather (position of the highest id per sequence), degradation-class scoring.

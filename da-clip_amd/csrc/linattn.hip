@@ -267,11 +267,9 @@ struct LaCfg {
   static constexpr int RB = C * ES;                      // x row bytes
   static constexpr int SL = RB / 16;                     // 16-byte slots per x row
   static constexpr int XT = TP * RB;                     // one x tile
-  static constexpr int ROW = TP * ES + 16;               // transposed P / V row (+pad)
-  static constexpr int PV = 2 * 32 * ROW;                // per wave: P and V
   static constexpr int QV = C / 4 / VE;                  // x vectors per thread (4 thr / px)
   static constexpr bool WREG = ES == 2;                  // weights cached in registers
-  static constexpr int SMEM = 2 * XT + 4 * PV + 4 * 64 * 4;
+  static constexpr int SMEM = 2 * XT + 4 * 64 * 4;      // x tiles + per-wave rescale scratch
   DEV static int swz(int row, int s) {                   // x tile slot swizzle
     const int f = SL >= 16 ? (row & 15) : SL == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
     return row * RB + ((s ^ f) << 4);
@@ -302,8 +300,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
   char* sx = smem;                                        // [2][TP][C] swizzled
   const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  char* sP = smem + 2 * K::XT + h * K::PV;                // this wave's [32][TP] P, then V
-  float* sm = reinterpret_cast<float*>(smem + 2 * K::XT + 4 * K::PV) + h * 64;
+  float* sm = reinterpret_cast<float*>(smem + 2 * K::XT) + h * 64;
   const int b = blockIdx.y, c = blockIdx.x;
   const int p0 = c * CH, p1 = min(HW, p0 + CH);
   float* out = part + ((size_t)b * nc + c) * LA_FPART;
@@ -410,49 +407,60 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
     };
     f32x4 acc[PT][4];                                     // k (0,1) | v (2,3)
     project(acc, 2, std::integral_constant<int, 4>{});
-    // ---- k: tile max per channel over valid pixels, online rescale.
+    // ---- k: tile max per channel over valid pixels, online rescale; then P = exp(k - m) and
+    // V straight from the projection accumulators: lane (lr, lg) holds channel lr of pixels
+    // pt*16 + lg*4 + r, which is itself a valid MFMA operand layout (row = channel, k = those
+    // pixels, the same pixel -> k map for P and V), so the context MFMA needs no LDS transpose.
+    // Padding pixels are 0. Whole tiles (all but an image's last) skip the validity tests.
     float sc[2];
-#pragma unroll
-    for (int jt = 0; jt < 2; ++jt) {
-      float m = -INFINITY;
-#pragma unroll
-      for (int pt = 0; pt < PT; ++pt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (t0 + pt * 16 + lg * 4 + r < p1) m = fmaxf(m, acc[pt][jt][r]);
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      const float mn = fmaxf(mrun[jt], m);
-      sc[jt] = exp_t<T>(mrun[jt] - mn);                   // 0 on the first tile
-      mrun[jt] = mn;
-      srun[jt] *= sc[jt];
-    }
-    // P = exp(k - m) and V straight from the projection accumulators: lane (lr, lg) holds
-    // channel lr of pixels pt*16 + lg*4 + r, which is itself a valid MFMA operand layout
-    // (row = channel, k = those pixels, the same pixel -> k map for P and V), so the context
-    // MFMA needs no LDS transpose. Padding pixels are 0.
     constexpr int PPK = KSTEP / 16;                       // pixel tiles per k-step: 2 bf16, 1 f32
     static_assert(PT % PPK == 0, "pixel tiles per k-step");
     u32x4 fp[2][PT / PPK], fv[2][PT / PPK];
+    auto kpv = [&](auto fullc) __attribute__((always_inline)) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int jt = 0; jt < 2; ++jt)
+      for (int jt = 0; jt < 2; ++jt) {
+        float m = -INFINITY;
 #pragma unroll
-      for (int kk = 0; kk < PT / PPK; ++kk) {
-        OpPack<T> pp, vp;
+        for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
-        for (int q = 0; q < PPK; ++q)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int pt = kk * PPK + q;
-            const bool ok = t0 + pt * 16 + lg * 4 + r < p1;
-            const float pe = ok ? exp_t<T>(acc[pt][jt][r] - mrun[jt]) : 0.f;
-            srun[jt] += pe;
-            pp.set(q * 4 + r, pe);
-            vp.set(q * 4 + r, ok ? acc[pt][2 + jt][r] : 0.f);
-          }
-        fp[jt][kk] = pp.get();
-        fv[jt][kk] = vp.get();
+          for (int r = 0; r < 4; ++r)
+            if (FULL || t0 + pt * 16 + lg * 4 + r < p1) m = fmaxf(m, acc[pt][jt][r]);
+        m = red16_max(m);
+        m = red32_max(m);
+        const float mn = fmaxf(mrun[jt], m);
+        sc[jt] = exp_t<T>(mrun[jt] - mn);                 // 0 on the first tile
+        mrun[jt] = mn;
+        srun[jt] *= sc[jt];
       }
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        // bf16: exp(k - m) = 2^(k log2e - m log2e), one v_fma + v_exp_f32.
+        const float ml = mrun[jt] * 1.4426950408889634f;
+#pragma unroll
+        for (int kk = 0; kk < PT / PPK; ++kk) {
+          OpPack<T> pp, vp;
+#pragma unroll
+          for (int q = 0; q < PPK; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int pt = kk * PPK + q;
+              const bool ok = FULL || t0 + pt * 16 + lg * 4 + r < p1;
+              float pe;
+              if constexpr (sizeof(T) == 2) pe = __builtin_amdgcn_exp2f(fmaf(acc[pt][jt][r], 1.4426950408889634f, -ml));
+              else pe = exp_t<T>(acc[pt][jt][r] - mrun[jt]);
+              if (!FULL) pe = ok ? pe : 0.f;
+              srun[jt] += pe;
+              pp.set(q * 4 + r, pe);
+              vp.set(q * 4 + r, ok ? acc[pt][2 + jt][r] : 0.f);
+            }
+          fp[jt][kk] = pp.get();
+          fv[jt][kk] = vp.get();
+        }
+      }
+    };
+    if (t0 + TP <= p1) kpv(std::true_type{});
+    else kpv(std::false_type{});
     // Broadcast the per-channel rescale factors to the ctx accumulator layout (row d).
     if (lg == 0) { sm[lr] = sc[0]; sm[16 + lr] = sc[1]; }
     wave_sync_lds();
@@ -487,8 +495,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
 #pragma unroll
   for (int jt = 0; jt < 2; ++jt) {
     float s = srun[jt];
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = red16_sum(s);
+    s = red32_sum(s);
     if (lg == 0) {
       out[4096 + h * 32 + jt * 16 + lr] = s;
       out[4096 + 128 + h * 32 + jt * 16 + lr] = mrun[jt];
@@ -568,8 +576,23 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
   constexpr int KS = C / KSTEP;                           // q-projection k-steps
   constexpr int KO = 128 / KSTEP;                         // out-GEMM k-steps
   constexpr int NH = C / 64;                              // 64-channel output halves
-  constexpr int WROW = C * ES + 16, EROW = 128 * ES + 16; // LDS rows (+16 B)
+  // LDS rows: 128- and 256-byte rows use an XOR slot swizzle (bank-conflict free for the
+  // {lr, lg} fragment reads: the +16 B padding it replaced was 2-way conflicted, 35 % of the
+  // LDS cycles); wider (fp32) rows keep the padding.
+  constexpr int QRB = C * ES, ERB = 128 * ES;
+  constexpr int WROW = (QRB == 128 || QRB == 256) ? QRB : QRB + 16;
+  constexpr int EROW = (ERB == 128 || ERB == 256) ? ERB : ERB + 16;
   constexpr int SMEM = 128 * WROW + C * EROW;
+  auto qoff = [](int row, int slot) {
+    if constexpr (QRB == 128) return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4);
+    else if constexpr (QRB == 256) return row * 256 + ((slot ^ (row & 15)) << 4);
+    else return row * WROW + (slot << 4);
+  };
+  auto eoff = [](int row, int slot) {
+    if constexpr (ERB == 128) return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4);
+    else if constexpr (ERB == 256) return row * 256 + ((slot ^ (row & 15)) << 4);
+    else return row * EROW + (slot << 4);
+  };
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char* sq = smem;                                        // Wq [128][C]
   char* sw = smem + 128 * WROW;                           // W_eff [C][128] permuted
@@ -589,13 +612,13 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
     constexpr int CPRQ = C / VE, CPRE = 128 / VE;
     for (int i = tid; i < 128 * CPRQ; i += 256) {
       const int r = i / CPRQ, cc = (i % CPRQ) * VE;
-      *reinterpret_cast<u32x4*>(sq + r * WROW + cc * ES) = *reinterpret_cast<const u32x4*>(w + (size_t)r * C + cc);
+      *reinterpret_cast<u32x4*>(sq + qoff(r, cc / VE)) = *reinterpret_cast<const u32x4*>(w + (size_t)r * C + cc);
     }
     const T* wb = weff + (size_t)b * C * 128;
     for (int i = tid; i < C * CPRE; i += 256) {
       const int p = i / CPRE, k0 = (i % CPRE) * VE;
       const int ch = (p & ~63) + la_perm<T>(p & 63);
-      T* dst = reinterpret_cast<T*>(sw + p * EROW + k0 * ES);
+      T* dst = reinterpret_cast<T*>(sw + eoff(p, k0 / VE));
       if constexpr (ES == 2) {
         const int s = k0 >> 5, l4 = ((k0 >> 3) & 3) * 4;
 #pragma unroll
@@ -637,16 +660,16 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
 #pragma unroll
       for (int j = 0; j < VE; ++j) { v[ks][j] = to_f(e[j]); s += v[ks][j]; }
     }
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
+    s = red16_sum(s);
+    s = red32_sum(s);
     const float mean = s * (1.f / (float)C);
     float qs = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < VE; ++j) { const float d = v[ks][j] - mean; qs += d * d; }
-    qs += __shfl_xor(qs, 16, 64);
-    qs += __shfl_xor(qs, 32, 64);
+    qs = red16_sum(qs);
+    qs = red32_sum(qs);
     const float rstd = rsq_t<T>(qs * (1.f / (float)C) + eps);
     u32x4 xf[KS];
 #pragma unroll
@@ -666,7 +689,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int jt = 0; jt < 8; ++jt) {
-        const u32x4 fw = *reinterpret_cast<const u32x4*>(sq + (jt * 16 + lr) * WROW + (ks * KSTEP + lg * VE) * ES);
+        const u32x4 fw = *reinterpret_cast<const u32x4*>(sq + qoff(jt * 16 + lr, (ks * KSTEP + lg * VE) / VE));
         Mma<T>::run(aq[jt], fw, xf[ks]);
       }
     // ---- softmax over head hd = channels of tiles 2hd, 2hd+1 (rows 4lg + r on this lane).
@@ -675,17 +698,28 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
       float m = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(aq[2 * hd][r], aq[2 * hd + 1][r]));
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      m = red16_max(m);
+      m = red32_max(m);
       float sm = 0.f;
+      if constexpr (ES == 2) {
+        // exp(a - m) = 2^(a log2e - m log2e): one v_fma + v_exp_f32 per element.
+        const float ml = m * 1.4426950408889634f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        aq[2 * hd][r] = exp_t<T>(aq[2 * hd][r] - m);
-        aq[2 * hd + 1][r] = exp_t<T>(aq[2 * hd + 1][r] - m);
-        sm += aq[2 * hd][r] + aq[2 * hd + 1][r];
+        for (int r = 0; r < 4; ++r) {
+          aq[2 * hd][r] = __builtin_amdgcn_exp2f(fmaf(aq[2 * hd][r], 1.4426950408889634f, -ml));
+          aq[2 * hd + 1][r] = __builtin_amdgcn_exp2f(fmaf(aq[2 * hd + 1][r], 1.4426950408889634f, -ml));
+          sm += aq[2 * hd][r] + aq[2 * hd + 1][r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          aq[2 * hd][r] = exp_t<T>(aq[2 * hd][r] - m);
+          aq[2 * hd + 1][r] = exp_t<T>(aq[2 * hd + 1][r] - m);
+          sm += aq[2 * hd][r] + aq[2 * hd + 1][r];
+        }
       }
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
+      sm = red16_sum(sm);
+      sm = red32_sum(sm);
       const float inv = rcp_t<T>(sm) * 0.17677669529663687f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) { aq[2 * hd][r] *= inv; aq[2 * hd + 1][r] *= inv; }
@@ -716,7 +750,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
       for (int hf = 0; hf < NH; ++hf)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const u32x4 fw = *reinterpret_cast<const u32x4*>(sw + (hf * 64 + j * 16 + lr) * EROW + (s2 * KSTEP + lg * VE) * ES);
+          const u32x4 fw = *reinterpret_cast<const u32x4*>(sw + eoff(hf * 64 + j * 16 + lr, (s2 * KSTEP + lg * VE) / VE));
           Mma<T>::run(acc[hf][j], fw, qf[s2]);
         }
     // ---- epilogue: o[ks][jj] is channel ks*KSTEP + lg*VE + jj of pixel px, the element x
@@ -734,16 +768,16 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
         o[ks][jj] = acc[hf][j][r] + bout[ks * KSTEP + lg * VE + jj];
         so += o[ks][jj];
       }
-    so += __shfl_xor(so, 16, 64);
-    so += __shfl_xor(so, 32, 64);
+    so = red16_sum(so);
+    so = red32_sum(so);
     const float mo = so * (1.f / (float)C);
     float qo = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int jj = 0; jj < VE; ++jj) { const float d = o[ks][jj] - mo; qo += d * d; }
-    qo += __shfl_xor(qo, 16, 64);
-    qo += __shfl_xor(qo, 32, 64);
+    qo = red16_sum(qo);
+    qo = red32_sum(qo);
     const float ro = 1.f / sqrtf(qo * (1.f / (float)C) + 1e-5f);
     if (px < p1) {
 #pragma unroll
@@ -778,8 +812,8 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
       ncu = 256;
   }
-  // Resident blocks per CU: 3 (C = 64, 3 waves / SIMD) or 2 (C = 128).
-  const int per_cu = (C == 64 ? 3 : 2) * (sizeof(T) == 2 ? 1 : 1);
+  // Resident blocks per CU (LDS-bound): 4 for bf16 C = 64 (32 KB of weights each), else 2.
+  const int per_cu = (C == 64 && sizeof(T) == 2) ? 4 : 2;
   int nb = (per_cu * ncu + B - 1) / B;
   nb = std::max(1, std::min(nb, (HW + 63) / 64));
   if (C == 64)

@@ -1,0 +1,30 @@
+"""Standalone timing of the SpatialTransformer attention core (dac_op_attention) at the UNet's
+32x32-level shapes: python tools/attn_bench.py [iters]. Prints us per call and TFLOP/s."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "da-clip_amd")]
+import torch  # noqa: E402
+from daclip_amd import _lib  # noqa: E402
+
+it = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+L_ = _lib.lib()
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+for (B, L, H) in [(8, 1024, 16), (8, 1024, 8)]:
+    qkv = torch.randn(B * L, 3 * H * 32, device="cuda").to(torch.bfloat16)
+    out = torch.empty(B * L, H * 32, device="cuda", dtype=torch.bfloat16)
+    for variant in (0, 1):
+        args = (ctypes.c_void_p(qkv.data_ptr()), ctypes.c_void_p(out.data_ptr()), B, L, H, _lib.DAC_BF16, variant, st)
+        for _ in range(3):
+            L_.dac_op_attention(*args)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(it):
+            L_.dac_op_attention(*args)
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / it
+        fl = 4.0 * B * H * L * L * 32
+        print(f"B={B} L={L} H={H} variant={variant}: {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
