@@ -379,8 +379,13 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     a.w2 = e.fuse1x1->w; a.w2_dual = e.fuse1x1->dual; a.bias2 = e.fuse1x1->b; a.y2 = e.y2; a.ldy2 = e.ldy2;
     fused = sizeof(T) == 2 && !use8 && a.w2 && cw.kh == 3 && stride == 1 && pad == 1 && !up &&
             e.fuse1x1->cout == cw.cout && e.fuse1x1->cin == cw.cin && conv_res_fusable(a);
-    if (!fused) { a.w2 = nullptr; a.bias2 = nullptr; a.y2 = nullptr; a.w2_dual = 0; a.ldy2 = 0; }
-    else fl += 2.0 * M * cw.cout * e.fuse1x1->cin_real;
+    if (!fused) {
+      a.w2 = nullptr; a.bias2 = nullptr; a.y2 = nullptr; a.w2_dual = 0; a.ldy2 = 0;
+      // Not fusable here: the 1x1 conv runs as its own launch (it only reads the same input).
+      conv_call<T>(r, *e.fuse1x1, x1, ld1, C1, x2, ld2, B, Hs, Ws, 0, 1, 0, e.y2, e.ldy2, Epi());
+    } else {
+      fl += 2.0 * M * cw.cout * e.fuse1x1->cin_real;
+    }
   }
   r.flops += fl;
   const int cls = cw.kh * 100 + (use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
@@ -418,8 +423,6 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     p->bytes += es * ((double)B * Hs * Ws * cw.cin_real + (double)cw.cout * cw.kh * cw.kw * cw.cin +
                       M * cw.cout * (1 + (e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0)));
   }
-  if (e.fuse1x1 && !fused)
-    conv_call<T>(r, *e.fuse1x1, x1, ld1, C1, x2, ld2, B, Hs, Ws, 0, 1, 0, e.y2, e.ldy2, Epi());
 }
 
 template <typename T>

@@ -504,35 +504,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
   }
 }
 
-// ctx[b] = sum_c part_c * exp(max_c - max_g) (rows d), sums likewise. 32 elements x 8 chunk
-// groups per block; the 8 group partials are combined in fixed order (deterministic).
+// ctx[b] = sum_c part_c * exp(max_c - max_g) (rows d), sums likewise. 16 elements x 16 chunk
+// groups per block, one pass per thread with an online max (rescale the running sum when a
+// chunk raises it); the 16 group partials are merged in fixed order (deterministic, and
+// independent of the batch).
 __global__ void __launch_bounds__(256) la_combine(const float* part, float* ctx, int nc) {
-  __shared__ float red[8][33];
-  const int b = blockIdx.y, el = threadIdx.x & 31, grp = threadIdx.x >> 5;
-  const int i = blockIdx.x * 32 + el;
+  __shared__ float rm[16][17], rs[16][17];
+  const int b = blockIdx.y, el = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + el;
   const bool live = i < LA_PART;
   const int d = !live ? 0 : i < 4096 ? i / 32 : i - 4096;
   const float* p = part + (size_t)b * nc * LA_FPART;
-  float mg = -INFINITY;
-  for (int c = grp; c < nc; c += 8) mg = fmaxf(mg, p[(size_t)c * LA_FPART + 4096 + 128 + d]);
-  red[grp][el] = mg;
-  __syncthreads();
-  mg = red[0][el];
-#pragma unroll
-  for (int k = 1; k < 8; ++k) mg = fmaxf(mg, red[k][el]);
-  __syncthreads();
-  float s = 0.f;
+  float m = -INFINITY, sum = 0.f;
   if (live)
-    for (int c = grp; c < nc; c += 8) {
+    for (int c = grp; c < nc; c += 16) {
       const float* q = p + (size_t)c * LA_FPART;
-      s += q[i] * expf(q[4096 + 128 + d] - mg);
+      const float mc = q[4096 + 128 + d], v = q[i];
+      if (mc == -INFINITY) continue;                 // empty chunk (all its terms are 0)
+      if (mc > m) {
+        sum = sum * expf(m - mc) + v;                // m = -inf on the first chunk: 0 * 0 + v
+        m = mc;
+      } else {
+        sum += v * expf(mc - m);
+      }
     }
-  red[grp][el] = s;
+  rm[grp][el] = m;
+  rs[grp][el] = sum;
   __syncthreads();
   if (grp == 0 && live) {
-    float t = red[0][el];
+    float mg = rm[0][el];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) t += red[k][el];
+    for (int k = 1; k < 16; ++k) mg = fmaxf(mg, rm[k][el]);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (rm[k][el] != -INFINITY) t += rs[k][el] * expf(rm[k][el] - mg);
     ctx[(size_t)b * LA_PART + i] = t;
   }
 }
@@ -803,7 +809,7 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
     la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
   else
     la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
-  la_combine<<<dim3((LA_PART + 31) / 32, B), 256, 0, st>>>(part, ctx, nc);
+  la_combine<<<dim3((LA_PART + 15) / 16, B), 256, 0, st>>>(part, ctx, nc);
   la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, 1.f / (float)HW);
   static int ncu = 0;
   if (!ncu) {
