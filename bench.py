@@ -28,7 +28,7 @@ HBM_PEAK = 8000.0                                  # GB/s
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
     (312, "bf16"): "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0EEEvNS_8ConvArgsEi",
-    (321, "bf16"): "void dac::conv3w_kernel<8>(dac::ConvArgs, int, int)",
+    (321, "bf16"): "void dac::conv3w_kernel<8, 4, 2>(dac::ConvArgs, int, int)",
     (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0EEEvNS_8ConvArgsEi",
     (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",

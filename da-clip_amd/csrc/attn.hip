@@ -422,52 +422,58 @@ void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, 
 }
 
 // ------------------------------------------------------------------------------ small MHA
-// Short-sequence MHA (ViT tokens L = 50 / 257, CLIP text L = 77), head dim 64 (or 32): one thread per
-// query, K / V of the (image, head) staged in LDS as fp32, single-pass online softmax (running
-// max + rescaled accumulator, so any L fits in registers); `causal` masks keys t > query
-// (the text tower's additive -inf upper triangle, transformer.py:751-757).
+// Short-sequence MHA (ViT tokens L = 50 / 257, CLIP text L = 77), head dim 64 (or 32): four
+// threads per query, each owning D/4 of the head dimensions (partial q.k dot products summed
+// over the quad with DPP), K / V of the (image, head) staged in LDS as fp32, single-pass online
+// softmax (running max + rescaled accumulator, so any L fits in registers); `causal` masks keys
+// t > query (the text tower's additive -inf upper triangle, transformer.py:751-757).
+template <int CTRL> DEV float dpp_quad(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 template <typename T, int D>
-__global__ void __launch_bounds__(64) small_mha_kernel(const T* __restrict__ qkv, T* o, int L, int H,
-                                                       int causal) {
+__global__ void __launch_bounds__(256) small_mha_kernel(const T* __restrict__ qkv, T* o, int L, int H,
+                                                        int causal) {
+  constexpr int DP = D / 4;                   // dims per thread
   extern __shared__ float sm[];               // K [L][D], V [L][D]
   const int b = blockIdx.y, h = blockIdx.x;
   const int ld = 3 * H * D;
   const T* base = qkv + (size_t)b * L * ld;
   float* sk = sm;
   float* sv = sm + L * D;
-  for (int i = threadIdx.x; i < L * (D / 4); i += 64) {
-    const int t = i / (D / 4), d = (i - t * (D / 4)) * 4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      sk[t * D + d + e] = to_f(base[(size_t)t * ld + H * D + h * D + d + e]);
-      sv[t * D + d + e] = to_f(base[(size_t)t * ld + 2 * H * D + h * D + d + e]);
-    }
+  for (int i = threadIdx.x; i < L * D; i += 256) {
+    const int t = i / D, d = i - t * D;
+    sk[i] = to_f(base[(size_t)t * ld + H * D + h * D + d]);
+    sv[i] = to_f(base[(size_t)t * ld + 2 * H * D + h * D + d]);
   }
   __syncthreads();
   const float scale = rsqrtf((float)D);
-  for (int qi = blockIdx.z * 64 + threadIdx.x; qi < L; qi += 64 * gridDim.z) {
-    float qv[D], acc[D];
+  const int part = threadIdx.x & 3, d0 = part * DP;
+  for (int qi = blockIdx.z * 64 + (threadIdx.x >> 2); qi < L; qi += 64 * gridDim.z) {
+    // (the quad's four lanes share qi, so the loop bound and the causal limit are quad-uniform)
+    float qv[DP], acc[DP];
 #pragma unroll
-    for (int d = 0; d < D; ++d) { qv[d] = to_f(base[(size_t)qi * ld + h * D + d]) * scale; acc[d] = 0.f; }
+    for (int d = 0; d < DP; ++d) { qv[d] = to_f(base[(size_t)qi * ld + h * D + d0 + d]) * scale; acc[d] = 0.f; }
     float mx = -INFINITY, sum = 0.f;
     const int tend = causal ? qi + 1 : L;
     for (int t = 0; t < tend; ++t) {
-      const float* kr = sk + t * D;
+      const float* kr = sk + t * D + d0;
       float a = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) a += qv[d] * kr[d];
+      for (int d = 0; d < DP; ++d) a += qv[d] * kr[d];
+      a += dpp_quad<0xB1>(a);                 // quad_perm [1,0,3,2]
+      a += dpp_quad<0x4E>(a);                 // quad_perm [2,3,0,1]
       const float mn = fmaxf(mx, a);
       const float c = expf(mx - mn), p = expf(a - mn);
       sum = sum * c + p;
-      const float* vr = sv + t * D;
+      const float* vr = sv + t * D + d0;
 #pragma unroll
-      for (int d = 0; d < D; ++d) acc[d] = acc[d] * c + p * vr[d];
+      for (int d = 0; d < DP; ++d) acc[d] = acc[d] * c + p * vr[d];
       mx = mn;
     }
     const float inv = 1.f / sum;
-    T* out = o + ((size_t)b * L + qi) * (H * D) + h * D;
+    T* out = o + ((size_t)b * L + qi) * (H * D) + h * D + d0;
 #pragma unroll
-    for (int d = 0; d < D; ++d) out[d] = from_f<T>(acc[d] * inv);
+    for (int d = 0; d < DP; ++d) out[d] = from_f<T>(acc[d] * inv);
   }
 }
 
@@ -475,8 +481,8 @@ template <typename T>
 void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal, hipStream_t st) {
   const size_t smem = (size_t)L * 2 * D * sizeof(float);
   const dim3 g(H, B, (L + 63) / 64);
-  if (D == 64) small_mha_kernel<T, 64><<<g, 64, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
-  else if (D == 32) small_mha_kernel<T, 32><<<g, 64, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
+  if (D == 64) small_mha_kernel<T, 64><<<g, 256, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
+  else if (D == 32) small_mha_kernel<T, 32><<<g, 256, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
   else __builtin_trap();
 }
 

@@ -13,6 +13,7 @@
 // XOR-swizzled by (row>>1)&7 so the 16 rows read by a ds_read_b128 lane group hit distinct
 // banks.
 #pragma once
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 #include "common.h"
@@ -1090,15 +1091,27 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
 // 16*((p>>2)&3) + 4*(p>>4) + (p&3), each lane's accumulators are 16 consecutive channels of
 // one pixel, so the epilogue runs from registers with 16-byte residual loads and stores.
 // Epilogue: (acc + bias) * (1 + scale) + shift -> SiLU -> + res1 + res2 + bbias (EPI_MIN).
+// Generalised over (NWV waves, TM = 16-pixel tiles per segment, NST ring stages per wave):
+// a deeper private ring keeps NST-1 stages' DMA in flight under the wave's MFMAs (the 2-stage
+// ring covered one stage of compute, less than an L2 round trip). LDS: 72 KB of weights +
+// NWV * NST * NI KB of rings (NI = DMA instructions of 16 halo rows per stage).
 constexpr int C3W_WAVES = 8;
 constexpr int C3W_WBYTES = 18 * 64 * 64;            // (chunk, kh, kw) regions of 64 rows x 64 B
-constexpr int C3W_STAGE = 80 * 64;                  // 5 DMA instructions of 16 halo rows
-template <int NWV>
+template <int NWV, int TM, int NST>
+struct C3W {
+  static constexpr int SEG = 16 * TM;               // output pixels per segment (tile)
+  static constexpr int NI = (SEG + 2 + 15) / 16;    // DMA instructions per stage
+  static constexpr int STAGE = NI * 1024;
+  static constexpr int SMEM = C3W_WBYTES + NWV * NST * STAGE;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+template <int NWV, int TM = 4, int NST = 2>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
-  constexpr int TM = 4, NF = TM + 2, VE = 8;
+  using CF = C3W<NWV, TM, NST>;
+  constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
   using SA = RowSwz<4, TM>;
   using SB = RowSwz<4, 1>;
-  __shared__ __attribute__((aligned(1024))) char smem[C3W_WBYTES + NWV * 2 * C3W_STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[CF::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, lg = lane >> 4;
@@ -1124,14 +1137,14 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
   int t = (int)((long)xcd * ntiles / 8) + (blockIdx.x >> 3) * NWV + wave;
   if (t >= t_end) return;
 
-  char* ring = smem + C3W_WBYTES + wave * 2 * C3W_STAGE;
+  char* ring = smem + C3W_WBYTES + wave * NST * STAGE;
   const char* wl = smem;
-  const int segs = a.Wo >> 6;
+  const int segs = a.Wo / SEG;
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   // Per-lane DMA geometry: instruction j fills physical halo row j*16 + lane/4.
-  int dr[5], dls[5];
+  int dr[NI], dls[NI];
 #pragma unroll
-  for (int j = 0; j < 5; ++j) {
+  for (int j = 0; j < NI; ++j) {
     const int R = SA::logical(j * 16 + (lane >> 2));
     dr[j] = R;
     dls[j] = SA::slot(R, lane & 3) * VE * 2;
@@ -1142,24 +1155,26 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 #pragma unroll
   for (int j = 0; j < 4; ++j) boff[j] = (16 * j + lr) * 64 + (SB::slot(16 * j + lr, lg) << 4);
 
-  // Stage (c, kh) of tile tt into ring buffer buf.
-  auto issue = [&](int tt, int c, int kh, int buf) {
-    const int rr = tt / segs, ow0 = (tt - rr * segs) << 6;
+  // Stage (c, kh) of tile tt into ring slot `slot`; tiles past this wave's range load the zero
+  // page so every stage issues exactly NI instructions (the counted waits rely on it).
+  auto issue = [&](int tt, int c, int kh, int slot) {
+    const bool live = tt < t_end;
+    const int rr = live ? tt / segs : 0, ow0 = live ? (tt - rr * segs) * SEG : 0;
     const int b = rr / a.Ho, oh = rr - b * a.Ho;
     const int ih = oh + kh - 1;
     const int ci0 = c * 32;
     const bool from1 = ci0 < a.C1;
     const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) + (size_t)(from1 ? ci0 : ci0 - a.C1) * 2;
     const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * 2;
-    const bool row_ok = (unsigned)ih < (unsigned)Hin;
+    const bool row_ok = live && (unsigned)ih < (unsigned)Hin;
     const int prow = b * a.Hs + (a.up ? (ih >> 1) : ih);
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < NI; ++j) {
       const int iw = ow0 + dr[j] - 1;
       const char* src = zero;
-      if (row_ok && dr[j] < 66 && (unsigned)iw < (unsigned)Win)
+      if (row_ok && dr[j] < SEG + 2 && (unsigned)iw < (unsigned)Win)
         src = xs + ((size_t)prow * a.Ws + (a.up ? (iw >> 1) : iw)) * ldb + dls[j];
-      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(ring + buf * C3W_STAGE + j * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(ring + slot * STAGE + j * 1024), 16, 0, 0);
     }
   };
 
@@ -1170,27 +1185,36 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 
   // Waves 4-7 share SIMDs with waves 0-3: start them about half a segment later, so one
   // wave's epilogue (VALU, SiLU transcendentals) overlaps its SIMD partner's MFMA phase.
-  if (wave & 4)
+  if (NWV > 4 && (wave & 4))
     for (int k = 0; k < delay; ++k) __builtin_amdgcn_s_sleep(8);
-  int buf = 0;
-  issue(t, 0, 0, 0);
+  // Global stage g = 6 * (tile index along this wave's walk) + (c * 3 + kh) lands in slot
+  // g % NST; stages g+1 .. g+NST-1 are in flight while g computes.
+#pragma unroll
+  for (int q = 0; q < NST - 1; ++q) issue(t + (q / 6) * stride, (q % 6) / 3, q % 3, q);
+  int slot = 0;
+  int g = 0;
   while (true) {
     const int tn = t + stride;
     const int rr = t / segs;
     const int b = rr / a.Ho;
-    const int m0 = rr * a.Wo + ((t - rr * segs) << 6);
+    const int m0 = rr * a.Wo + (t - rr * segs) * SEG;
     f32x4 acc[TM][4];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
+    for (int s = 0; s < 6; ++s, ++g) {
       const int c = s / 3, kh = s % 3;
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      if (s < 5) issue(t, (s + 1) / 3, (s + 1) % 3, buf ^ 1);
-      else if (tn < t_end) issue(tn, 0, 0, buf ^ 1);
-      const char* st = ring + buf * C3W_STAGE;
+      // Own DMA of stage g landed: NST-2 younger stages (NI instructions each) may stay in
+      // flight (epilogue loads / stores issued since only make this wait longer).
+      if constexpr (NST == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((NST - 2) * NI) : "memory");
+      {
+        const int sn = s + NST - 1;                   // stage to issue: (tile + sn/6, sn%6)
+        issue(t + (sn / 6) * stride, (sn % 6) / 3, sn % 3, (slot + NST - 1) % NST);
+      }
+      const char* st = ring + slot * STAGE;
       u32x4 fa[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) fa[f] = *reinterpret_cast<const u32x4*>(st + aoff[f]);
@@ -1205,7 +1229,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 #pragma unroll
           for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[j], fa[i + kw]);
       }
-      buf ^= 1;
+      slot = slot + 1 == NST ? 0 : slot + 1;
     }
     // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15.
     epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; });
@@ -1215,7 +1239,18 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-inline int conv3w_blocks(int ntiles) {
+// Kernel shape of the 64 -> 64 3x3 convs: DAC_C3W=<waves>,<TM>,<stages> (tuning), default
+// 8 waves x 64-pixel segments x 2 stages.
+struct C3WCfg { int nwv = 8, tm = 4, nst = 2; };
+inline C3WCfg c3w_cfg() {
+  static C3WCfg c = [] {
+    C3WCfg r;
+    if (const char* e = getenv("DAC_C3W")) sscanf(e, "%d,%d,%d", &r.nwv, &r.tm, &r.nst);
+    return r;
+  }();
+  return c;
+}
+inline int conv3w_blocks(int ntiles, int nwv) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1223,9 +1258,26 @@ inline int conv3w_blocks(int ntiles) {
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
       ncu = 256;
   }
-  int nb = (ntiles + C3W_WAVES - 1) / C3W_WAVES;
+  int nb = (ntiles + nwv - 1) / nwv;
   if (nb > ncu) nb = ncu;
   return (nb + 7) / 8 * 8;                          // whole XCD bands
+}
+inline void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
+  const C3WCfg c = c3w_cfg();
+#define DAC_C3W(NW_, TM_, NS_)                                                                 \
+  if (c.nwv == NW_ && c.tm == TM_ && c.nst == NS_ && a.Wo % (16 * TM_) == 0) {                  \
+    const int ntiles = a.B * a.Ho * (a.Wo / (16 * TM_));                                        \
+    conv3w_kernel<NW_, TM_, NS_><<<conv3w_blocks(ntiles, NW_), 64 * NW_, 0, st>>>(a, ntiles, delay); \
+    return;                                                                                     \
+  }
+  DAC_C3W(8, 2, 3)
+  DAC_C3W(8, 2, 2)
+  DAC_C3W(4, 4, 4)
+  DAC_C3W(4, 4, 3)
+  DAC_C3W(6, 4, 2)
+#undef DAC_C3W
+  const int ntiles = a.B * a.Ho * (a.Wo >> 6);
+  conv3w_kernel<C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
 }
 
 template <typename T, int KH, int KW, int S, int P>
@@ -1257,9 +1309,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && std::is_same<T, bf16>::value) {
     if ((g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) {
-      const int ntiles = a.B * a.Ho * (a.Wo >> 6);
       const int delay = g_conv3_force >= 30 ? (g_conv3_force - 30) * 2 : 6;   // swept: 4-10 best
-      conv3w_kernel<C3W_WAVES><<<conv3w_blocks(ntiles), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+      conv3w_launch(a, delay, st);
       return;
     }
   }
