@@ -27,7 +27,9 @@ HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
-    (312, "bf16"): "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0EEEvNS_8ConvArgsEi",
+    # class 312 = v4 256x64 swapped-operand tiles, plain and with the fused res_conv output
+    (312, "bf16"): ("_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0EEEvNS_8ConvArgsEi",
+                    "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi28ELi0EEEvNS_8ConvArgsEi"),
     (321, "bf16"): "void dac::conv3w_kernel<8, 4, 2>(dac::ConvArgs, int, int)",
     (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0EEEvNS_8ConvArgsEi",
     (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
@@ -39,12 +41,23 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def pmc_entry(kernel_id, dtype):
-    """Per-dispatch PMC figures of the timed kernel (same bench workload), or None."""
-    sym = KERNEL_SYMBOL.get((kernel_id, dtype))
-    if sym is None or not os.path.exists(PMC_FILE):
+    """Per-dispatch PMC figures of the timed kernel class (same bench workload), or None. A
+    class served by several kernel symbols is averaged over their dispatches."""
+    syms = KERNEL_SYMBOL.get((kernel_id, dtype))
+    if syms is None or not os.path.exists(PMC_FILE):
         return None
+    if isinstance(syms, str):
+        syms = (syms,)
     with open(PMC_FILE) as f:
-        return json.load(f)["kernels"].get(sym)
+        ks = json.load(f)["kernels"]
+    es = [ks[s] for s in syms if s in ks and "hbm_bytes_per_dispatch" in ks[s]]
+    if not es:
+        return None
+    n = sum(e["dispatches"] for e in es)
+    out = {"dispatches": n, "hbm_bytes_per_dispatch": sum(e["hbm_bytes_total"] for e in es) / n}
+    if all("mfma_busy" in e for e in es):
+        out["mfma_busy"] = sum(e["mfma_busy"] * e["dispatches"] for e in es) / n
+    return out
 
 
 def parse():

@@ -103,8 +103,18 @@ DEV void perm16_swap(float& a, float& b) { asm("s_nop 1\n\tv_permlane16_swap_b32
 DEV void perm32_swap(float& a, float& b) { asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b)); }
 DEV float red16_sum(float v) { float a = v, b = v; perm16_swap(a, b); return a + b; }
 DEV float red32_sum(float v) { float a = v, b = v; perm32_swap(a, b); return a + b; }
-DEV float red16_max(float v) { float a = v, b = v; perm16_swap(a, b); return fmaxf(a, b); }
-DEV float red32_max(float v) { float a = v, b = v; perm32_swap(a, b); return fmaxf(a, b); }
+// The max is taken inside the asm too: an fmaxf on asm outputs makes the compiler canonicalize
+// both operands first (two extra v_max x,x); the inputs here are already canonical values.
+DEV float red16_max(float v) {
+  float a = v, b = v;
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_max_f32 %0, %0, %1" : "+v"(a), "+v"(b));
+  return a;
+}
+DEV float red32_max(float v) {
+  float a = v, b = v;
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_max_f32 %0, %0, %1" : "+v"(a), "+v"(b));
+  return a;
+}
 
 DEV float wave_sum(float v) {
 #pragma unroll
