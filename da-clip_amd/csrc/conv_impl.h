@@ -1218,16 +1218,22 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
       u32x4 fa[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) fa[f] = *reinterpret_cast<const u32x4*>(st + aoff[f]);
+      // Weight fragments double-buffered across the kw taps: tap kw+1's reads are in flight
+      // under tap kw's MFMAs.
+      const char* wr0 = wl + (c * 3 + kh) * 3 * 4096;
+      u32x4 fw[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fw[0][j] = *reinterpret_cast<const u32x4*>(wr0 + boff[j]);
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const char* wr = wl + ((c * 3 + kh) * 3 + kw) * 4096;
-        u32x4 fw[4];
+        if (kw < 2) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fw[j] = *reinterpret_cast<const u32x4*>(wr + boff[j]);
+          for (int j = 0; j < 4; ++j) fw[(kw + 1) & 1][j] = *reinterpret_cast<const u32x4*>(wr0 + (kw + 1) * 4096 + boff[j]);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[j], fa[i + kw]);
+          for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[kw & 1][j], fa[i + kw]);
       }
       slot = slot + 1 == NST ? 0 : slot + 1;
     }
@@ -1351,6 +1357,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         // Rows of 32 (the 32x32 level), Cout <= 256: 128x64 tiles of 32-pixel wave tiles
         // (TM = 2), 8 % faster than v3 in the UNet; the 512-wide convs stay on v3 (v4 with
         // 128x128 tiles measured 3-4 % slower there).
+        // (The 512-wide convs stay on v3: v4 128x64 swapped tiles measured 11 % faster in
+        // convbench but 3 % slower in the network.)
         if constexpr (sizeof(T) == 2)
           if (a.Cout <= 256 && a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st)) return;
         if (a.Cout <= 256 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 4>(a, st)) return;
@@ -1445,6 +1453,18 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
               return;
             }
           DAC_V2(64, 128, 2, 2, 3, 256)
+        case 14:
+        case 15:
+        case 16:
+          if constexpr (sizeof(T) == 2)
+            if (minimal(128) && a.Cout % 128 == 0) {
+              dim3 g((Mg + 127) / 128, a.Cout / 128, gz);
+              if (f2 == 14) conv2_kernel<T, 128, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP><<<g, 256, 0, st>>>(a);
+              else if (f2 == 15) conv2_kernel<T, 128, 128, 2, 2, 3, KH, KW, S, P, EPI_SWAP><<<g, 256, 0, st>>>(a);
+              else conv2_kernel<T, 64, 128, 2, 2, 4, KH, KW, S, P, EPI_SWAP><<<dim3((Mg + 63) / 64, a.Cout / 128, gz), 256, 0, st>>>(a);
+              return;
+            }
+          DAC_V2(64, 128, 2, 2, 2, 256)
         default: break;
       }
     }

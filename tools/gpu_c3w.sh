@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-for cfg in 8,4,2 8,2,3 8,2,2 4,4,4 4,4,3 6,4,2; do
+for cfg in ${CFGS:-8,4,2 8,4,-3}; do
   echo "== $cfg" 
   DAC_C3W=$cfg timeout -k 10 60 ./tools/convbench 2 "64->64" check || exit 1
   DAC_C3W=$cfg timeout -k 10 60 ./tools/convbench 50 "64->64" || exit 1
