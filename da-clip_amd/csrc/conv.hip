@@ -23,7 +23,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // interleaved-row tiles) 256x64, 13 = v2 7x7 row-tap layout (bf16, Cin = 8), 14 = v4 256x16
 // (narrow Cout), 15 / 16 / 17 / 18 = v2 1x1 128x256 (GEGLU) / 256x256 / 64x128 / 128x64,
 // 2-stage, 20 = v4 with 32-pixel wave tiles 128x64, 21 = v5 weight-stationary 3x3 (64 -> 64),
-// 22 / 23 = conv_edge.hip init_conv (7x7, Cin 8, Cout 64) / final_conv (3x3, Cout <= 4).
+// 22 / 23 = conv_edge.hip init_conv (7x7, Cin 8, Cout 64) / final_conv (3x3, Cout <= 4),
+// 24 = conv_down.hip (4x4 stride-2 Downsample).
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -43,6 +44,7 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
                        (!a.res1 || a.ldr1 % VEh == 0) && (!a.res2 || a.ldr2 % VEh == 0);
   if (kh == 7 && elem_bytes == 2 && conv7_ok(a)) return 22;
   if (kh == 3 && elem_bytes == 2 && g_conv3_force < 0 && conv3n_ok(a)) return 23;
+  if (kh == 4 && elem_bytes == 2 && g_conv3_force < 0 && conv_down_ok(a)) return 24;
   if (kh == 7 && elem_bytes == 2 && a.Cin == 8 && a.K == 7 * 8 * 8 && a.zero && a.amode == 0 && !batched &&
       !a.x2)
     return 13;

@@ -1320,6 +1320,12 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       return;
     }
   }
+  if constexpr (KH == 4 && KW == 4 && S == 2 && P == 1 && sizeof(T) == 2) {
+    if (g_conv3_force < 0 && conv_down_ok(a)) {
+      conv_down(a, st);
+      return;
+    }
+  }
   if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
     if (conv7_ok(a)) {
       conv7(a, st);

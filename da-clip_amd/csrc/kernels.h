@@ -74,6 +74,10 @@ void conv7(const ConvArgs& a, hipStream_t st);
 // streaming kernel with hi/lo as separate MFMA rows (conv_edge.hip).
 bool conv3n_ok(const ConvArgs& a);
 void conv3n(const ConvArgs& a, hipStream_t st);
+// Downsample (4x4, stride 2, pad 1, bf16, Cin % 32 == 0, Cout % 64 == 0): row-band tiles with
+// deinterleaved even / odd input pixels (conv_down.hip).
+bool conv_down_ok(const ConvArgs& a);
+void conv_down(const ConvArgs& a, hipStream_t st);
 int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 
 // fp8 (e4m3, MX block scales) implicit GEMM for bf16 activations (conv8.hip): w8 [Cout][Kp]

@@ -81,16 +81,22 @@ __global__ void __launch_bounds__(256) la_ctx(const T* __restrict__ qkv, const f
   constexpr int KSTEP = Mma<T>::KSTEP;
   __shared__ __attribute__((aligned(16))) char sP[128 * ROW];
   __shared__ __attribute__((aligned(16))) char sV[128 * ROW];
-  __shared__ float gmax[128];
+  __shared__ float gmax[2][128];
   __shared__ float sred[PP][128];
 
   const int b = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, h = tid >> 6, lr = lane & 15, lg = lane >> 4;
-  if (tid < 128) {
+  {
+    // Global per-channel max over the chunk maxima: two threads per channel, unrolled so the
+    // loads overlap (one dependent load per chunk cost ~10 us at nc = 64).
+    const int ch = tid & 127, half = tid >> 7;
     float m = -INFINITY;
-    for (int i = 0; i < nc; ++i) m = fmaxf(m, pmax[((size_t)b * nc + i) * 128 + tid]);
-    gmax[tid] = m;
+#pragma unroll 8
+    for (int i = half; i < nc; i += 2) m = fmaxf(m, pmax[((size_t)b * nc + i) * 128 + ch]);
+    gmax[half][ch] = m;
   }
+  __syncthreads();
+  if (tid < 128) gmax[0][tid] = fmaxf(gmax[0][tid], gmax[1][tid]);
   __syncthreads();
   const int cv = tid % NV2, pr = tid / NV2;
   const bool isk = cv < NV2 / 2;
@@ -98,7 +104,7 @@ __global__ void __launch_bounds__(256) la_ctx(const T* __restrict__ qkv, const f
   char* dst = isk ? sP : sV;
   float gm[VE], ssum[VE];
 #pragma unroll
-  for (int e = 0; e < VE; ++e) { gm[e] = isk ? gmax[c0 + e] : 0.f; ssum[e] = 0.f; }
+  for (int e = 0; e < VE; ++e) { gm[e] = isk ? gmax[0][c0 + e] : 0.f; ssum[e] = 0.f; }
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -164,14 +170,27 @@ __global__ void __launch_bounds__(256) la_ctx(const T* __restrict__ qkv, const f
   }
 }
 
+// Sum of the chunk partials: 32 elements x 8 chunk groups per block, the group sums merged
+// in fixed order (deterministic; the chunking depends only on HW).
 __global__ void __launch_bounds__(256) la_reduce(const float* part, float* ctx, int nc) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= LA_PART) return;
-  const float* p = part + (size_t)b * nc * LA_PART + i;
+  __shared__ float red[8][33];
+  const int b = blockIdx.y, el = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + el;
+  const bool live = i < LA_PART;
   float s = 0.f;
-  for (int c = 0; c < nc; ++c) s += p[(size_t)c * LA_PART];
-  ctx[(size_t)b * LA_PART + i] = s;
+  if (live) {
+    const float* p = part + (size_t)b * nc * LA_PART + i;
+#pragma unroll 4
+    for (int c = grp; c < nc; c += 8) s += p[(size_t)c * LA_PART];
+  }
+  red[grp][el] = s;
+  __syncthreads();
+  if (grp == 0 && live) {
+    float t = red[0][el];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) t += red[k][el];
+    ctx[(size_t)b * LA_PART + i] = t;
+  }
 }
 
 template <typename T>
@@ -197,7 +216,7 @@ void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B
   float* ctx = pmax + (size_t)B * nc * 128;
   la_kmax<T><<<dim3(nc, B), 256, 0, st>>>((const T*)qkv, pmax, HW, nc, CH);
   la_ctx<T><<<dim3(nc, B), 256, 0, st>>>((const T*)qkv, pmax, part, HW, nc, CH);
-  la_reduce<<<dim3((LA_PART + 255) / 256, B), 256, 0, st>>>(part, ctx, nc);
+  la_reduce<<<dim3((LA_PART + 31) / 32, B), 256, 0, st>>>(part, ctx, nc);
   la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, 1.f / (float)HW);
 }
 

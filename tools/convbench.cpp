@@ -237,6 +237,9 @@ int main(int argc, char** argv) {
     {"L0 7x7 8->64 init", 8, 256, 256, 8, 64, 7, 1, 3, 0, 0, 0, 0, 8},
     {"L0 7x7 8->64 init v1", 8, 256, 256, 8, 64, 7, 1, 3, 0, 0, 0, 0, 0},
     {"L0 3x3 64->3 final", 8, 256, 256, 64, 3, 3, 1, 1, 0, 0, 0, 0, 0, 1},
+    {"L0 4x4s2 64->64 down", 8, 256, 256, 64, 64, 4, 2, 1, 0, 0, 0, 0, 0, 1},
+    {"L1 4x4s2 64->128 down", 8, 128, 128, 64, 128, 4, 2, 1, 0, 0, 0, 0, 0, 1},
+    {"L2 4x4s2 128->256 down", 8, 64, 64, 128, 256, 4, 2, 1, 0, 0, 0, 0, 0, 1},
   };
   size_t maxe = (size_t)8 * 256 * 256 * 512;
   void *x, *y, *w, *res, *zero; float *ss, *bias;
