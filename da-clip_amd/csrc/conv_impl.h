@@ -1488,7 +1488,18 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       // plain outputs 256x256 (8 waves of 64x128, 2 stages, minimal epilogue only: the
       // general one spills at this tile); the rest 64x128 with 2 stages (4 waves of 32x64),
       // which doubles the blocks of the small 32x32-level GEMMs over 128x128.
-      if (a.act == ACT_GEGLU) DAC_V2(128, 256, 2, 4, 2, 512)
+      if (a.act == ACT_GEGLU) {
+        // 256x256 tiles when they stay inside one image: half the LDS-DMA bytes per MFMA of
+        // the 128x256 tiles, whose per-stage refill the MFMAs could not cover.
+        if constexpr (sizeof(T) == 2)
+          if (rows_ok && !a.res1 && !a.res2 && !a.bbias && (batched || HWo % 256 == 0) && a.Cout % 256 == 0 &&
+              g_conv2_force == 0) {
+            dim3 g((Mg + 255) / 256, a.Cout / 256, gz);
+            conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_GEGLU><<<g, 512, 0, st>>>(a);
+            return;
+          }
+        DAC_V2(128, 256, 2, 4, 2, 512)
+      }
       if (a.Cout >= 1024 && minimal(256)) {
         dim3 g((Mg + 255) / 256, (a.Cout + 255) / 256, gz);
         conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_MIN><<<g, 512, 0, st>>>(a);

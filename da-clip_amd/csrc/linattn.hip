@@ -524,40 +524,43 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
 }
 
 // ctx[b] = sum_c part_c * exp(max_c - max_g) (rows d), sums likewise. 16 elements x 16 chunk
-// groups per block, one pass per thread with an online max (rescale the running sum when a
-// chunk raises it); the 16 group partials are merged in fixed order (deterministic, and
-// independent of the batch).
+// groups per block; every thread loads its (at most 8) chunks' values and maxima up front, the
+// global max is reduced through LDS, then each group sums its terms and the 16 group sums are
+// merged in fixed order (deterministic; the chunking depends only on HW).
 __global__ void __launch_bounds__(256) la_combine(const float* part, float* ctx, int nc) {
-  __shared__ float rm[16][17], rs[16][17];
+  constexpr int NG = 16, PER = 8;                 // la_chunks() <= 128 = NG * PER
+  __shared__ float red[NG][17];
   const int b = blockIdx.y, el = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int i = blockIdx.x * 16 + el;
   const bool live = i < LA_PART;
   const int d = !live ? 0 : i < 4096 ? i / 32 : i - 4096;
   const float* p = part + (size_t)b * nc * LA_FPART;
-  float m = -INFINITY, sum = 0.f;
-  if (live)
-    for (int c = grp; c < nc; c += 16) {
-      const float* q = p + (size_t)c * LA_FPART;
-      const float mc = q[4096 + 128 + d], v = q[i];
-      if (mc == -INFINITY) continue;                 // empty chunk (all its terms are 0)
-      if (mc > m) {
-        sum = sum * expf(m - mc) + v;                // m = -inf on the first chunk: 0 * 0 + v
-        m = mc;
-      } else {
-        sum += v * expf(mc - m);
-      }
-    }
-  rm[grp][el] = m;
-  rs[grp][el] = sum;
+  float mc[PER], v[PER];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = grp + NG * k;
+    const bool ok = live && c < nc;
+    mc[k] = ok ? p[(size_t)c * LA_FPART + 4096 + 128 + d] : -INFINITY;
+    v[k] = ok ? p[(size_t)c * LA_FPART + i] : 0.f;
+    m = fmaxf(m, mc[k]);
+  }
+  red[grp][el] = m;
+  __syncthreads();
+  float mg = red[0][el];
+#pragma unroll
+  for (int g = 1; g < NG; ++g) mg = fmaxf(mg, red[g][el]);
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (mc[k] != -INFINITY) sum += v[k] * expf(mc[k] - mg);
+  red[grp][el] = sum;
   __syncthreads();
   if (grp == 0 && live) {
-    float mg = rm[0][el];
+    float t = red[0][el];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) mg = fmaxf(mg, rm[k][el]);
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (rm[k][el] != -INFINITY) t += rs[k][el] * expf(rm[k][el] - mg);
+    for (int g = 1; g < NG; ++g) t += red[g][el];
     ctx[(size_t)b * LA_PART + i] = t;
   }
 }

@@ -23,11 +23,20 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
   float v[NVL][VE];
   float s = 0.f;
   const bool live = row < rows;
+  // Gain / bias / residual loads go out with the row (they do not depend on the statistics),
+  // so their latency overlaps the reductions instead of following them.
+  float gv[NVL][VE], bv[NVL][VE], rv[NVL][VE];
 #pragma unroll
   for (int j = 0; j < NVL; ++j) {
     const int idx = sub + G * j;
     if (live && idx < NV) {
       load_vec<T>(x + (size_t)row * ldx + idx * VE, v[j]);
+      if (res) load_vec<T>(res + (size_t)row * ldr + idx * VE, rv[j]);
+#pragma unroll
+      for (int e = 0; e < VE; e += 4) {
+        load_vec<float>(g + idx * VE + e, gv[j] + e);
+        if (b) load_vec<float>(b + idx * VE + e, bv[j] + e);
+      }
 #pragma unroll
       for (int e = 0; e < VE; ++e) s += v[j][e];
     }
@@ -52,18 +61,12 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
   for (int j = 0; j < NVL; ++j) {
     const int idx = sub + G * j;
     if (idx >= NV) continue;
-    float o[VE], r[VE], gv[VE], bv[VE];
-    if (res) load_vec<T>(res + (size_t)row * ldr + idx * VE, r);
-#pragma unroll
-    for (int e = 0; e < VE; e += 4) {
-      load_vec<float>(g + idx * VE + e, gv + e);
-      if (b) load_vec<float>(b + idx * VE + e, bv + e);
-    }
+    float o[VE];
 #pragma unroll
     for (int e = 0; e < VE; ++e) {
-      float t = (v[j][e] - mean) * rstd * gv[e];
-      if (b) t += bv[e];
-      if (res) t += r[e];
+      float t = (v[j][e] - mean) * rstd * gv[j][e];
+      if (b) t += bv[j][e];
+      if (res) t += rv[j][e];
       o[e] = t;
     }
     store_vec<T>(y + (size_t)row * ldy + idx * VE, o);
