@@ -83,9 +83,15 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   return a.Cout <= 64 ? 1 : 2;
 }
 
+// The fused res_conv rides on the bf16 v4 swapped-operand kernels: 256x64 tiles (variant 12)
+// or, for 32-pixel rows (the 32x32 level, any Cout), 128x64 tiles.
 bool conv_res_fusable(const ConvArgs& a) {
-  return a.w2 && a.y2 && a.ldy2 % 8 == 0 && a.bias2 == nullptr && conv_variant(a, 3, 2) == 12 &&
-         a.Cout % 64 == 0;
+  if (!(a.w2 && a.y2 && a.ldy2 % 8 == 0 && a.bias2 == nullptr && a.Cout % 64 == 0)) return false;
+  const int v = conv_variant(a, 3, 2);
+  if (v == 12) return true;
+  if (v != 20 && v != 7 && v != 11) return false;     // 128x64 v4 / v3 candidates only
+  const bool kok = (a.C1 >= a.Cin || a.C1 % 32 == 0) && a.Cin % 32 == 0;
+  return kok && conv3_rw_host(a, 128) > 0 && conv3_rw_host(a, 128) % 32 == 0;
 }
 
 template <typename T>

@@ -1355,6 +1355,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         if constexpr (sizeof(T) == 2) {
           if (a.y2) {
             if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
+            if (a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
           } else if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) {
             return;
           }
