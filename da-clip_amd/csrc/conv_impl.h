@@ -201,33 +201,61 @@ DEV int wperm64(int p) { return 16 * ((p >> 2) & 3) + 4 * (p >> 4) + (p & 3); }
 // LN = true (to_out of LinearAttention, Cout = 64 in one wave): row LayerNorm over the 64
 // channels held by lanes lr, lr+16, lr+32, lr+48 (two xor shuffles), gain ln_g, after the bias
 // and before the residual (module_util.py:77-86, 180-185).
-template <int TM, bool LN = false, class PixOf>
-DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
-                    const PixOf& pix) {
+// Operands of a register epilogue loaded ahead: a persistent kernel issues them before the
+// next tile's first DMA, so waiting for them never waits for that DMA (vmcnt retires in issue
+// order). One register set holds either the residual rows (res1) or, on convs without one,
+// the per-image scale/shift rows (ss) — the UNet's block2 and block1 convs respectively.
+template <int TM> struct EpiPref { u32x4 v[2 * TM > 8 ? 2 * TM : 8]; };
+// The loads are inline asm the compiler cannot see: its wait insertion treats vmcnt as out of
+// order once loads, stores and LDS-DMA are all pending, and would put a vmcnt(0) — a wait for
+// the next tile's DMA too — ahead of the first use. The caller waits with a counted vmcnt
+// instead (these loads are older than every DMA issued after them), before any use.
+DEV void ld_asm(u32x4& r, const void* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+}
+template <int TM, class PixOf>
+DEV void epi_prefetch(const ConvArgs& a, int nb, int b, const PixOf& pix, EpiPref<TM>& p) {
+  // One set of loads whatever the operand (addresses selected, not branches): per-branch
+  // destinations would be merged by register copies, reading registers still in flight.
+  constexpr int N = 2 * TM > 8 ? 2 * TM : 8;
+  if (!a.res1 && !a.ss) return;
   const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
-  const bf16* r2 = reinterpret_cast<const bf16*>(a.res2);
+  const float* s4 = a.ss + (size_t)b * a.ss_ld + nb;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const int i = k / 2 < TM ? k / 2 : TM - 1, q = k & 7;
+    const void* src = r1 ? (const void*)(r1 + pix(i) * a.ldr1 + nb + 8 * (k & 1))
+                         : (const void*)(s4 + (q < 4 ? 4 * q : a.Cout + 4 * (q - 4)));
+    ld_asm(p.v[k], src);
+  }
+}
+
+// PRE: operands come from epi_prefetch and the conv has no bbias / res2 / (ss with res1) —
+// the epilogue then issues no loads at all, so it never waits for in-flight DMA.
+template <int TM, bool LN = false, bool PRE = false, class PixOf>
+DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
+                    const PixOf& pix, const EpiPref<TM>* pre = nullptr) {
   bf16* y = reinterpret_cast<bf16*>(a.y);
   __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
-  u32x4 rv[TM][2];
-  if (r1) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) rv[i][h] = *reinterpret_cast<const u32x4*>(r1 + pix(i) * a.ldr1 + nb + 8 * h);
-  }
   float sc[16], sh[16];
   if (a.ss) {
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
-    const f32x4* h4 = reinterpret_cast<const f32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
+    const u32x4* h4 = reinterpret_cast<const u32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 u = s4[q], w = h4[q];
+      u32x4 u, w;
+      if constexpr (PRE) { u = pre->v[q]; w = pre->v[4 + q]; } else { u = s4[q]; w = h4[q]; }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { sc[4 * q + e] = u[e] + 1.f; sh[4 * q + e] = w[e]; }
+      for (int e = 0; e < 4; ++e) { sc[4 * q + e] = __uint_as_float(u[e]) + 1.f; sh[4 * q + e] = __uint_as_float(w[e]); }
     }
   } else {
 #pragma unroll
     for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
+  }
+  float bb[16];
+  if (!PRE && a.bbias) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bb[e] = a.bbias[(size_t)b * a.bb_ld + nb + e];
   }
   float gl[16];
   if constexpr (LN) {
@@ -260,22 +288,30 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
       for (int e = 0; e < 16; ++e) v[e] = (v[e] - mean) * rstd * gl[e];
     }
-    float t1[8];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (r1) {
-        const bf16* e1 = reinterpret_cast<const bf16*>(&rv[i][h]);
+      if (a.res1) {
+        const u32x4 r1 = PRE ? pre->v[2 * i + h]
+                             : *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(a.res1) + m * a.ldr1 + nb + 8 * h);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += (float)e1[e];
+        for (int w = 0; w < 4; ++w) {              // bf16 pair -> two floats by bit shifts (no spills)
+          const unsigned u = r1[w];
+          v[8 * h + 2 * w] += __uint_as_float(u << 16);
+          v[8 * h + 2 * w + 1] += __uint_as_float(u & 0xffff0000u);
+        }
       }
-      if (r2) {
-        load_vec<bf16>(r2 + m * a.ldr2 + nb + 8 * h, t1);
+      if (!PRE && a.res2) {
+        const u32x4 r2 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(a.res2) + m * a.ldr2 + nb + 8 * h);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += t1[e];
+        for (int w = 0; w < 4; ++w) {
+          const unsigned u = r2[w];
+          v[8 * h + 2 * w] += __uint_as_float(u << 16);
+          v[8 * h + 2 * w + 1] += __uint_as_float(u & 0xffff0000u);
+        }
       }
-      if (a.bbias) {
+      if (!PRE && a.bbias) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[8 * h + e] += a.bbias[(size_t)b * a.bb_ld + nb + 8 * h + e];
+        for (int e = 0; e < 8; ++e) v[8 * h + e] += bb[8 * h + e];
       }
       store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
     }
@@ -1203,13 +1239,21 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    EpiPref<TM> pref;
 #pragma unroll
     for (int s = 0; s < 6; ++s, ++g) {
       const int c = s / 3, kh = s % 3;
       // Own DMA of stage g landed: NST-2 younger stages (NI instructions each) may stay in
-      // flight (epilogue loads / stores issued since only make this wait longer).
-      if constexpr (NST == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((NST - 2) * NI) : "memory");
+      // flight. At a tile's first stage the previous tile's epilogue issued its 2*TM 16-byte
+      // stores after this stage's DMA (vmcnt retires in issue order), so those may stay in
+      // flight too instead of stalling the wave for a store round trip.
+      if constexpr (NST == 2) {
+        if (s == 0 && g > 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * TM) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((NST - 2) * NI) : "memory");
+      }
+      if (s == 5) epi_prefetch<TM>(a, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, pref);
       {
         const int sn = s + NST - 1;                   // stage to issue: (tile + sn/6, sn%6)
         issue(t + (sn / 6) * stride, (sn % 6) / 3, sn % 3, (slot + NST - 1) % NST);
@@ -1237,8 +1281,10 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
       }
       slot = slot + 1 == NST ? 0 : slot + 1;
     }
-    // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15.
-    epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; });
+    // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15. The
+    // prefetched operands landed once at most the next tile's first stage (NI DMA) is pending.
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
+    epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, &pref);
     if (tn >= t_end) break;
     t = tn;
   }

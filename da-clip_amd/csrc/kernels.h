@@ -62,7 +62,7 @@ inline bool conv3w_ok(const ConvArgs& a) {
   return a.Cin == 64 && a.Cout == 64 && a.K == 576 && a.cwrap == 0 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
          !a.ln_g && (a.act == ACT_NONE || a.act == ACT_SILU) && a.Wo >= 64 && a.Wo % 64 == 0 &&
          (a.C1 >= a.Cin || a.C1 % 32 == 0) && a.ldy % 8 == 0 && a.ld1 % 8 == 0 &&
-         (a.C1 >= a.Cin || a.ld2 % 8 == 0) && (!a.res1 || a.ldr1 % 8 == 0) && (!a.res2 || a.ldr2 % 8 == 0);
+         (a.C1 >= a.Cin || a.ld2 % 8 == 0) && (!a.res1 || a.ldr1 % 8 == 0) && !a.res2 && !a.bbias && !(a.ss && a.res1);   // (epi_regs16 PRE)
 }
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
