@@ -767,8 +767,8 @@ template <int SLOTS, int TM> struct RowSwz {
 // FL bit 0: sched_barrier fences around each stage (MFMAs stay inside their stage, so the
 // stage's DMA wait overlaps them instead of preceding them); bit 1: all B fragments of a stage
 // are read up front.
-template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN>
-__global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
+__global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 conv3i_kernel(ConvArgs a, int RW) {
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
@@ -904,6 +904,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   // kh must be a compile-time index into a_pix (a dynamic index sends the table to scratch).
   auto issue = [&](int c, auto khc, int buf) {
     constexpr int kh = decltype(khc)::value;
+    if constexpr ((FL & 32) != 0) return;                       // diagnostic: no DMA
     char* st = smem + buf * STAGE;
     const int ci0 = c * BKE;
     const bool from1 = ci0 < a.C1;
@@ -1006,7 +1007,8 @@ conv3i_kernel(ConvArgs a, int RW) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int jn = 0; jn < TN; ++jn) {
-            if constexpr (SWAP) Mma<T>::run(acc[i][jn], fb[jn], fa[i + kw]);
+            if constexpr ((FL & 64) != 0) acc[i][jn][0] += __uint_as_float(fb[jn][0] ^ fa[i + kw][0]);  // diagnostic: no MFMA
+            else if constexpr (SWAP) Mma<T>::run(acc[i][jn], fb[jn], fa[i + kw]);
             else Mma<T>::run(acc[i][jn], fa[i + kw], fb[jn]);
           }
       }
@@ -1077,13 +1079,13 @@ extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 
-template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN>
+template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   constexpr int WTM = BM / WGM, BKE = CK / sizeof(T);
   const int RW = conv3_rw(a, BM);
   if (RW <= 0 || RW % WTM || a.Cin % BKE || (a.C1 < a.Cin && a.C1 % BKE)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
-  conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
+  conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
   return true;
 }
 template <typename T>
@@ -1110,6 +1112,12 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
       return false;
     case 41:
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st);
+      return false;
+    case 42:   // diagnostics (convbench only; results are garbage): 40 without DMA / without MFMA
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32>(a, st);
+      return false;
+    case 43:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 64>(a, st);
       return false;
     default: return false;
   }
