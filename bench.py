@@ -28,10 +28,10 @@ HBM_PEAK = 8000.0                                  # GB/s
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
     # class 312 = v4 256x64 swapped-operand tiles, plain and with the fused res_conv output
-    (312, "bf16"): ("_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0EEEvNS_8ConvArgsEi",
-                    "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi28ELi0EEEvNS_8ConvArgsEi"),
+    (312, "bf16"): ("_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0ELi2EEEvNS_8ConvArgsEi",
+                    "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi28ELi0ELi2EEEvNS_8ConvArgsEi"),
     (321, "bf16"): "void dac::conv3w_kernel<8, 4, 2>(dac::ConvArgs, int, int)",
-    (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0EEEvNS_8ConvArgsEi",
+    (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0ELi2EEEvNS_8ConvArgsEi",
     (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (306, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",

@@ -804,7 +804,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   static_assert(VMW < 64, "vmcnt");
   // FL bit 3: swapped MFMA operands (weights as A) + register epilogue (epi_regs16).
   constexpr bool SWAP = (FL & 8) != 0;
-  static_assert(!SWAP || (WGN == 1 && BN == 64 && sizeof(T) == 2 && EPK == EPI_MIN), "swapped tiles");
+  static_assert(!SWAP || (WTN == 64 && sizeof(T) == 2 && EPK == EPI_MIN && (!RES || BN == 64)), "swapped tiles");
   // Whole-tile epilogue (one pass, residual prefetch) whenever its fp32 tile still leaves room
   // for two blocks per CU; otherwise passes that fit in the pipeline's LDS.
   constexpr int EPR = EpiLds<BM, BN>::BYTES <= 80 * 1024 ? BM : epi_rows<BM, BN, WTM>(ST * STAGE);
@@ -856,7 +856,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   for (int j = 0; j < BGX; ++j) {
     const int row = (wave + j * NW) * RPI + lane / SLOTS;
     b_ls[j] = SB::slot(row, lane % SLOTS) * VE;
-    const int n = n0 + (SWAP ? wperm64(row % BN) : row % BN);
+    const int n = n0 + (SWAP ? (row % BN & ~63) + wperm64(row % BN & 63) : row % BN);
     b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
                           : nullptr;
   }
@@ -1050,7 +1050,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
   if constexpr (SWAP) {
-    const int nb = n0 + 16 * lg;
+    const int nb = n0 + wn * WTN + 16 * lg;
     float bi[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
