@@ -1030,7 +1030,7 @@ conv3i_kernel(ConvArgs a, int RW) {
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
     if (s + ST - 2 < S) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VMW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((FL & 256) == 0) __builtin_amdgcn_s_barrier();   // (FL 256: diagnostic, no barrier)
     asm volatile("" ::: "memory");
     if (s + ST - 1 < S) issue(c + CN, std::integral_constant<int, KN>{}, nbuf);
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
@@ -1049,6 +1049,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
+  if constexpr ((FL & 128) != 0) {                 // diagnostic: no epilogue (all MFMA chains kept live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1.2345e-30f) reinterpret_cast<float*>(a.y)[tid] = t;
+    return;
+  }
   if constexpr (SWAP) {
     const int nb = n0 + wn * WTN + 16 * lg;
     float bi[16];
@@ -1118,6 +1127,18 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
       return false;
     case 43:
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 64>(a, st);
+      return false;
+    case 44:   // diagnostics: no DMA and no epilogue / no DMA and no barrier / both / no epilogue
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32 | 128>(a, st);
+      return false;
+    case 45:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32 | 256>(a, st);
+      return false;
+    case 46:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32 | 128 | 256>(a, st);
+      return false;
+    case 47:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 128>(a, st);
       return false;
     default: return false;
   }
