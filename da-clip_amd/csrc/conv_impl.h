@@ -1023,6 +1023,17 @@ conv3i_kernel(ConvArgs a, int RW) {
   if constexpr (ST >= 3) issue(0, std::integral_constant<int, 1>{}, 1);
   if constexpr (ST >= 4) issue(0, std::integral_constant<int, 2>{}, 2);
   int buf = 0, nbuf = ST - 1;
+  // Swapped tiles without the fused res_conv: the epilogue's residual or scale/shift rows are
+  // loaded at the start of the last stage (inline asm, so they stay there), landing under its
+  // MFMAs instead of after them (the fused variant has no registers left for them).
+  const bool pre_ok = SWAP && !RES && !a.res2 && !a.bbias && !(a.ss && a.res1) &&
+                      (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0));
+  EpiPref<TM> pref;
+  const int rm_base = b * HWo + oh0 * a.Wo + ow0;
+  auto pixf = [&](int i) {
+    const int t = wm * WTM + TM * lr + i;
+    return (size_t)(rm_base + (t >> rws) * a.Wo + (t & ((1 << rws) - 1)));
+  };
   auto step = [&](int c, auto khc) {
     constexpr int kh = decltype(khc)::value;
     constexpr int KN = (kh + ST - 1) % 3, CN = (kh + ST - 1) / 3;
@@ -1033,6 +1044,12 @@ conv3i_kernel(ConvArgs a, int RW) {
     if constexpr ((FL & 256) == 0) __builtin_amdgcn_s_barrier();   // (FL 256: diagnostic, no barrier)
     asm volatile("" ::: "memory");
     if (s + ST - 1 < S) issue(c + CN, std::integral_constant<int, KN>{}, nbuf);
+    if constexpr (SWAP && kh == 2) {
+      if (s + 1 == S && pre_ok) {
+        const int nb = n0 + wn * WTN + 16 * lg;
+        epi_prefetch<TM>(a, nb, b, pixf, pref);
+      }
+    }
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
     compute(buf, khc);
     buf = buf + 1 == ST ? 0 : buf + 1;
@@ -1061,9 +1078,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   if constexpr (SWAP) {
     const int nb = n0 + wn * WTN + 16 * lg;
     float bi[16];
+    if (pre_ok) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-    epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); });
+      for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+      epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+      epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); });
+    }
     if constexpr (RES) {
       // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
       bf16* y2 = reinterpret_cast<bf16*>(a.y2);
