@@ -234,11 +234,21 @@ DEV void epi_prefetch(const ConvArgs& a, int nb, int b, const PixOf& pix, EpiPre
 // the epilogue then issues no loads at all, so it never waits for in-flight DMA.
 template <int TM, bool LN = false, bool PRE = false, class PixOf>
 DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
-                    const PixOf& pix, const EpiPref<TM>* pre = nullptr) {
+                    const PixOf& pix, const EpiPref<TM>* pre = nullptr, const float* ssl = nullptr) {
   bf16* y = reinterpret_cast<bf16*>(a.y);
   __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
+  if constexpr (PRE) {
+    // Every prefetched register stays allocated until here (after the caller's wait), also the
+    // ones this epilogue does not read (TM < 4 duplicates): a register freed earlier could be
+    // reused while its load is still in flight and then be overwritten when the load lands.
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(pre->v) / sizeof(pre->v[0])); ++k) asm volatile("" :: "v"(pre->v[k]));
+  }
   float sc[16], sh[16];
-  if (a.ss) {
+  if (a.ss && ssl) {                             // scale / shift rows staged in LDS by the caller
+#pragma unroll
+    for (int e = 0; e < 16; ++e) { sc[e] = ssl[e] + 1.f; sh[e] = ssl[64 + e]; }
+  } else if (a.ss) {
     const u32x4* s4 = reinterpret_cast<const u32x4*>(a.ss + (size_t)b * a.ss_ld + nb);
     const u32x4* h4 = reinterpret_cast<const u32x4*>(a.ss + (size_t)b * a.ss_ld + a.Cout + nb);
 #pragma unroll
@@ -808,7 +818,10 @@ conv3i_kernel(ConvArgs a, int RW) {
   // Whole-tile epilogue (one pass, residual prefetch) whenever its fp32 tile still leaves room
   // for two blocks per CU; otherwise passes that fit in the pipeline's LDS.
   constexpr int EPR = EpiLds<BM, BN>::BYTES <= 80 * 1024 ? BM : epi_rows<BM, BN, WTM>(ST * STAGE);
-  constexpr int SMEM = ((FL & 8) || ST * STAGE > EpiLds<EPR, BN>::BYTES) ? ST * STAGE : EpiLds<EPR, BN>::BYTES;
+  // Swapped tiles: 1 KB after the ring holds the tile's per-image scale / shift rows and bias
+  // (64 channels each), DMA'd with the first stage, read by the epilogue from LDS.
+  constexpr int SMEM = (FL & 8) ? ST * STAGE + 1024
+                       : (ST * STAGE > EpiLds<EPR, BN>::BYTES ? ST * STAGE : EpiLds<EPR, BN>::BYTES);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   using SA = RowSwz<SLOTS, TM>;
   using SB = RowSwz<SLOTS, 1>;
@@ -1020,14 +1033,23 @@ conv3i_kernel(ConvArgs a, int RW) {
   // stage issued at (c, kh) is s + ST - 1 = (c + (kh + ST - 1) / 3, (kh + ST - 1) % 3).
   const int nchunk = a.Cin / BKE, S = 3 * nchunk;
   issue(0, std::integral_constant<int, 0>{}, 0);
+  if constexpr (SWAP) {
+    if (wave == 0) {                              // lanes 0-15 scale, 16-31 shift, 32-47 bias
+      const int part = lane >> 4, l16 = lane & 15;
+      const float* src = reinterpret_cast<const float*>(zero);
+      if (part == 0 && a.ss) src = a.ss + (size_t)b * a.ss_ld + n0 + 4 * l16;
+      else if (part == 1 && a.ss) src = a.ss + (size_t)b * a.ss_ld + a.Cout + n0 + 4 * l16;
+      else if (part == 2 && a.bias) src = a.bias + n0 + 4 * l16;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + ST * STAGE), 16, 0, 0);
+    }
+  }
   if constexpr (ST >= 3) issue(0, std::integral_constant<int, 1>{}, 1);
   if constexpr (ST >= 4) issue(0, std::integral_constant<int, 2>{}, 2);
   int buf = 0, nbuf = ST - 1;
-  // Swapped tiles without the fused res_conv: the epilogue's residual or scale/shift rows are
-  // loaded at the start of the last stage (inline asm, so they stay there), landing under its
-  // MFMAs instead of after them (the fused variant has no registers left for them).
-  const bool pre_ok = SWAP && !RES && !a.res2 && !a.bbias && !(a.ss && a.res1) &&
-                      (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0));
+  // Swapped tiles without the fused res_conv: the epilogue's residual rows are loaded at the
+  // start of the last stage (inline asm, so they stay there), landing under its MFMAs instead of
+  // after them (the fused variant has no registers left for them).
+  const bool pre_ok = SWAP && !RES && a.res1 && !a.res2 && !a.bbias && !a.ss;
   EpiPref<TM> pref;
   const int rm_base = b * HWo + oh0 * a.Wo + ow0;
   auto pixf = [&](int i) {
@@ -1078,15 +1100,11 @@ conv3i_kernel(ConvArgs a, int RW) {
   if constexpr (SWAP) {
     const int nb = n0 + wn * WTN + 16 * lg;
     float bi[16];
-    if (pre_ok) {
+    const float* el = reinterpret_cast<const float*>(smem + ST * STAGE) + 16 * lg;   // LDS terms
 #pragma unroll
-      for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-      epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-      epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); });
-    }
+    for (int e = 0; e < 16; ++e) bi[e] = el[128 + e];
+    if (pre_ok) epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
+    else epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
     if constexpr (RES) {
       // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
       bf16* y2 = reinterpret_cast<bf16*>(a.y2);
@@ -1116,6 +1134,8 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   constexpr int WTM = BM / WGM, BKE = CK / sizeof(T);
   const int RW = conv3_rw(a, BM);
   if (RW <= 0 || RW % WTM || a.Cin % BKE || (a.C1 < a.Cin && a.C1 % BKE)) return false;
+  if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
+    if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
   conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
   return true;
