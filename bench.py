@@ -152,33 +152,44 @@ def cpu_baseline(args, sd_unet, sd_clip):
                       f"per-image time = encode + {args.T} x step"}
 
 
-def psnr_vs_reference(args, clip, unet, dev):
-    """PSNR parity of the benchmarked mode against the REFERENCE CPU path: the headline fixture
-    (tests/golden/headline_256_t100.npz, made by running the reference's predict.py flow on
-    images/00006.jpg with the same seeded weights and injected noise) is restored by this
-    run's own encoder + UNet handles (B=1, 256^2, T=100). delta_db = PSNR(ours, LQ) -
-    PSNR(reference, LQ) (no GT exists for the image); north-star bar |delta_db| < 1e-3."""
-    from daclip_amd import synth
+def psnr_vs_reference(args, clip, dev):
+    """PSNR parity of the benchmarked mode against the REFERENCE CPU path on a real restoration:
+    tests/golden/restore_rain_256_t100.npz is the reference's predict.py flow run in the
+    fixture builder on the 256x256 centre crop of images/3_rain.png (BASELINE configs[0]) with
+    the tracking UNet weights of synth.tracking_state_dict (the reference's loop converges,
+    98.5 % of its output in (0,1), 27.1 dB vs the LQ) and injected noise. It is restored here
+    by this run's encoder handle and a UNet handle of the benchmarked dtype loaded with those
+    weights (B=1, 256^2, T=100). delta_db = PSNR(ours, LQ) - PSNR(reference, LQ) on uint8
+    (no GT exists for the image); north-star bar |delta_db| < 1e-3."""
+    from daclip_amd import arch, synth
+    from daclip_amd.unet import ConditionalUNet
     from daclip_amd.sde import IRSDE
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     t0 = time.perf_counter()
-    g = np.load(os.path.join(ROOT, "tests", "golden", "headline_256_t100.npz"))
+    g = np.load(os.path.join(ROOT, "tests", "golden", "restore_rain_256_t100.npz"))
+    sd = synth.tracking_state_dict(synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), 0),
+                                   g["w_g1"], g["w_g2"], float(g["k"]))
+    u = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype=args.dtype)
+    u.load_state_dict(sd)
     lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0).to(dev)
-    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=71, tag="hl_noise_state")).to(dev)
-    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=72, tag="hl_steps")).to(dev)
+    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=91, tag="rs_noise_state")).to(dev)
+    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=92, tag="rs_steps")).to(dev)
     ic, dc = clip.encode_image(torch.from_numpy(g["img4clip"]).to(dev), control=True)
     s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
-    s.set_model(unet)
+    s.set_model(u)
     s.set_mu(lq)
     out = s.reverse_posterior(s.noise_state(lq, noise=ns), noises=zs, text_context=dc, image_context=ic)
     u8 = tensor2img(out[0])
     ref = g["out"][0]
     o = out[0].cpu().numpy()
-    return {"vs": "reference CPU path (tests/golden/headline_256_t100.npz: predict.py flow, images/00006.jpg, "
-                  "same seeded weights + injected noise)",
+    inr = (ref > 0) & (ref < 1)
+    return {"vs": "reference CPU path (tests/golden/restore_rain_256_t100.npz: predict.py flow on the "
+                  "images/3_rain.png 256x256 crop, tracking UNet weights, injected noise)",
             "delta_db": round(float(calculate_psnr(u8, g["lq_u8"]) - calculate_psnr(g["out_u8"], g["lq_u8"])), 6),
             "psnr_vs_reference_u8_db": round(float(calculate_psnr(u8, g["out_u8"])), 3),
-            "out_max_rel_err": float(np.abs(o - ref).max() / np.abs(ref).max()),
+            "u8_mismatch": round(float(np.mean(u8 != g["out_u8"])), 5),
+            "inrange_max_abs_err": float(np.abs(o - ref)[inr].max()),
+            "reference_inrange_frac": round(float(inr.mean()), 4),
             "sample": f"B=1 256x256 T=100 restore in the benchmarked dtype ({time.perf_counter() - t0:.1f}s)"}
 
 
@@ -300,7 +311,7 @@ def main():
     psnr = None
     if rank == 0 and not args.no_psnr:
         if args.model == "universal-ir" and args.T == 100:
-            psnr = psnr_vs_reference(args, clip, unet, dev)
+            psnr = psnr_vs_reference(args, clip, dev)
         elif args.dtype == "bf16":
             psnr = psnr_sample(args, wu_keys=uspec, clip=clip, unet_bf16=unet, lq=lq[:1], img=img4clip[:1], dev=dev)
 

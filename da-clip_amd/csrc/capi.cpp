@@ -158,7 +158,7 @@ int dac_encode_image(dac_handle* h, const float* img, int B, float* image_ctx, f
                      void* stream) {
   return guard(h, [&]() -> int {
     need_ready(h);
-    if (!img || !image_ctx || !degra_ctx || B < 1) throw dac::Error(DAC_E_ARG, "bad argument");
+    if (!img || !image_ctx || B < 1) throw dac::Error(DAC_E_ARG, "bad argument");
     h->eng->encode(img, B, image_ctx, degra_ctx, (hipStream_t)stream);
     return DAC_OK;
   });

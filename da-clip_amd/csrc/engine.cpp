@@ -1092,13 +1092,16 @@ struct VitNet {
       small_linear(pf, D, tw.projT, nullptr, out, E, B, D, E, ACT_NONE, ACT_NONE, nullptr, 0, 1, r.st);
     }
   }
-  void encode(Run& r, const float* img, int B, float* ic, float* dc) {
+  // control: DaCLIP.encode_image(control=True) (daclip_model.py:46-53), the controller tower
+  // and then the clip tower with its hiddens; otherwise CLIP.encode_image (daclip_model.py:54-55
+  // -> model.py:233-235), the clip tower alone.
+  void encode(Run& r, const float* img, int B, float* ic, float* dc, bool control) {
     constexpr int VE = sizeof(T) == 2 ? 8 : 4;
     T* xin = r.alloc<T>((size_t)B * S * S * VE);
     if (!r.dry) vit_prep<T>(img, xin, B, S, r.st);
     std::vector<const void*> hid;
-    tower(r, ctl, xin, B, true, &hid, nullptr, dc);
-    tower(r, main, xin, B, false, nullptr, &hid, ic);
+    if (control) tower(r, ctl, xin, B, true, &hid, nullptr, dc);
+    tower(r, main, xin, B, false, nullptr, control ? &hid : nullptr, ic);
   }
 };
 
@@ -1246,11 +1249,11 @@ class EngineT : public Engine {
     Run d;
     d.dry = true;
     d.ar = &a;
-    vit->encode(d, nullptr, B, nullptr, nullptr);
+    vit->encode(d, nullptr, B, nullptr, nullptr, dc != nullptr);
     ensure_arena(a.peak + (1 << 20));
     Run r = live(st);
     arena.reset();
-    vit->encode(r, img, B, ic, dc);
+    vit->encode(r, img, B, ic, dc, dc != nullptr);
     HIP_OK(hipGetLastError());
   }
 
@@ -1425,7 +1428,7 @@ class EngineT : public Engine {
     Run r;
     r.dry = true;
     r.ar = &a;
-    vit->encode(r, nullptr, B, nullptr, nullptr);
+    vit->encode(r, nullptr, B, nullptr, nullptr, true);
     return r.flops;
   }
 

@@ -8,6 +8,7 @@ native ConditionalUNet (libdaclip_hip), so `sde.set_model(model.model)` makes
 IRSDE.reverse_posterior run the whole loop as one captured hipGraph.
 
 Deliberate differences, all additive:
+  * test() takes optional injected per-step noises (the reference draws randn_like);
   * get_current_visuals() also returns "Outputs" / "GTs" with the whole batch (the reference
     keeps element 0 only, denoising_model.py:170-172);
   * checkpoints are read with torch.load(weights_only=True) (nothing executes from the file);
@@ -77,15 +78,17 @@ class DenoisingModel:
         self.text_context = text_context
         self.image_context = image_context
 
-    def test(self, sde=None, mode="posterior", save_states=False):
+    def test(self, sde=None, mode="posterior", save_states=False, noises=None):
+        """denoising_model.py:152-162. `noises` ([T,B,C,H,W], optional) replaces the sampler's
+        per-step randn_like draws (parity tests inject the reference's noise)."""
         sde.set_mu(self.condition)
         with torch.no_grad():
             if mode == "sde":
-                self.output = sde.reverse_sde(self.state, save_states=save_states,
+                self.output = sde.reverse_sde(self.state, save_states=save_states, noises=noises,
                                               text_context=self.text_context,
                                               image_context=self.image_context)
             elif mode == "posterior":
-                self.output = sde.reverse_posterior(self.state, save_states=save_states,
+                self.output = sde.reverse_posterior(self.state, save_states=save_states, noises=noises,
                                                     text_context=self.text_context,
                                                     image_context=self.image_context)
             else:

@@ -112,9 +112,10 @@ class DaCLIP:
         return self
 
     def encode_image(self, image: torch.Tensor, control: bool = False, normalize: bool = False):
-        """daclip_model.py:46-55 -> (image_features, degra_features) [B, embed_dim] fp32."""
-        if not control:
-            raise NotImplementedError("encode_image(control=False) (plain CLIP) is off the hot path")
+        """daclip_model.py:46-55. control=True -> (image_features, degra_features), the
+        controller's hiddens injected into the clip tower; control=False (the reference's
+        default) -> CLIP.encode_image (model.py:233-235): the clip tower's features alone.
+        [B, embed_dim] fp32."""
         if not self._loaded:
             raise RuntimeError("DaCLIP: weights not loaded")
         img = image.to(self.device, torch.float32).contiguous()
@@ -123,11 +124,13 @@ class DaCLIP:
         if tuple(img.shape[1:]) != (3, s, s):
             raise RuntimeError(f"expected [B,3,{s},{s}], got {tuple(img.shape)}")
         ic = torch.empty((B, self.vision.embed_dim), device=self.device, dtype=torch.float32)
-        dc = torch.empty_like(ic)
+        dc = torch.empty_like(ic) if control else None
         h = self._h
         with torch.cuda.device(self.device):
             h.check(_lib.lib().dac_encode_image(h.h, _lib._ptr(img), B, _lib._ptr(ic), _lib._ptr(dc),
                                                 h.stream()), "encode_image")
+        if not control:
+            return torch.nn.functional.normalize(ic, dim=-1) if normalize else ic
         if normalize:
             ic = torch.nn.functional.normalize(ic, dim=-1)
             dc = torch.nn.functional.normalize(dc, dim=-1)

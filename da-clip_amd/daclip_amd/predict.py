@@ -7,7 +7,10 @@ encode_image(control=True) -> noise_state -> feed_data -> test(sde) -> tensor2im
 
 `predict_batch` restores B images in one pass (one encode + one captured loop for the whole
 batch) and returns all of them; images must share one size. With no checkpoint on the box,
-`synthetic=True` loads the seeded synthetic weights of both networks.
+`synthetic=True` loads the seeded synthetic weights of both networks (`synthetic_clip` alone
+keeps a UNet checkpoint from opt while the encoder is synthetic). Both predict entry points
+take optional injected noises (the noise_state draw and the per-step draws) so the chain can
+be pinned against the reference run with the same noises.
 """
 from __future__ import annotations
 
@@ -31,13 +34,14 @@ def imread_bgr(path: str) -> np.ndarray:
 
 class Predictor:
     def setup(self, opt: Union[str, dict], daclip_path: Optional[str] = None, device="cuda",
-              dtype: str = "fp32", synthetic: bool = False) -> None:
+              dtype: str = "fp32", synthetic: bool = False,
+              synthetic_clip: Optional[bool] = None) -> None:
         opt = parse_options(opt) if isinstance(opt, str) else dict(opt)
         if synthetic:
             opt["path"] = dict(opt.get("path") or {}, pretrain_model_G=None)
         self.model = create_model(opt, device=device, dtype=dtype)
         self.device = self.model.device
-        if synthetic:
+        if synthetic if synthetic_clip is None else synthetic_clip:
             self.clip_model = open_clip.create_model("daclip_ViT-B-32", device=self.device, dtype=dtype)
             self.clip_model.load_synthetic(0)
         else:
@@ -56,17 +60,21 @@ class Predictor:
             ic, dc = self.clip_model.encode_image(img4clip, control=True)
         return ic.float(), dc.float()
 
-    def predict_batch(self, images_bgr: Sequence[np.ndarray]) -> List[np.ndarray]:
+    def predict_batch(self, images_bgr: Sequence[np.ndarray], noise: Optional[torch.Tensor] = None,
+                      noises: Optional[torch.Tensor] = None) -> List[np.ndarray]:
+        """predict.py:62-91 for B same-size images. `noise` [B,3,H,W] / `noises` [T,B,3,H,W]
+        optionally replace the noise_state and per-step randn_like draws."""
         rgb = [im[:, :, [2, 1, 0]] / 255.0 for im in images_bgr]
         ic, dc = self._contexts(rgb)
         lq = torch.stack([torch.tensor(im, dtype=torch.float32).permute(2, 0, 1) for im in rgb])
-        noisy = self.sde.noise_state(lq)
+        noisy = self.sde.noise_state(lq, noise=noise)
         self.model.feed_data(noisy, lq, text_context=dc, image_context=ic)
-        self.model.test(self.sde, mode=self.mode)
+        self.model.test(self.sde, mode=self.mode, noises=noises)
         out = self.model.get_current_visuals(need_GT=False)["Outputs"]
         return [tensor2img(o) for o in out]
 
-    def predict(self, image: Union[str, np.ndarray]) -> np.ndarray:
+    def predict(self, image: Union[str, np.ndarray], noise: Optional[torch.Tensor] = None,
+                noises: Optional[torch.Tensor] = None) -> np.ndarray:
         """One image (path or BGR uint8 HWC) -> restored BGR uint8 HWC."""
         im = imread_bgr(image) if isinstance(image, str) else image
-        return self.predict_batch([im])[0]
+        return self.predict_batch([im], noise=noise, noises=noises)[0]

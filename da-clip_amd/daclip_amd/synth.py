@@ -63,3 +63,79 @@ def synth_images(n: int, h: int, w: int, seed: int = 0) -> np.ndarray:
 
 def synth_noise(shape: Iterable[int], seed: int = 0, tag: str = "noise") -> np.ndarray:
     return _rng(seed, tag).standard_normal(tuple(shape)).astype(np.float32)
+
+
+# --------------------------------------------------------------------------- tracking weights
+TRACK_T = 100
+TRACK_KNOTS = np.arange(0, 256, 2)[:TRACK_T]      # time-embedding dims carrying the t hinges
+TRACK_GAMMA = 10.0                                # hinge slope per unit t
+
+
+def tracking_state_dict(sd: Mapping[str, np.ndarray], w_g1: np.ndarray, w_g2: np.ndarray,
+                        k: float) -> Dict[str, np.ndarray]:
+    """Synthetic nf=64 UNet weights (ch_mult [1,2,4,8], context 512) under which the reference's
+    T=100 posterior loop restores instead of diverging (the restoration fixture,
+    tests/golden/make_golden.py gen_restore). With random weights eps does not track
+    (x - mu)/sigma_bar_t, so the posterior's (x - mu) coefficient (~1.11 per step at t ~ 100,
+    sde_utils.py:205-213, 245-247) multiplies up to 1/eps = 200 and the output saturates.
+    These weights make the network predict
+
+        eps = g1(t) (x - mu) - g2(t) D,    g1 = 1/sigma_bar_t,  g2 = exp(-theta_cumsum_t dt)/sigma_bar_t
+
+    so that x0 = mu + D, where D = k * (3x3 projection A of the 64 deep-path channels entering
+    final_res_block): every down / mid / up kernel shapes the output. Inside the architecture
+    (DenoisingUNet_arch.py:118-174):
+      * init_conv channels 0..2 copy xt - cond (7x7 centre tap 1);
+      * time_mlp dims TRACK_KNOTS carry hinges GELU(GAMMA (i + 3/2 - t)), i = 0..T-1, from the
+        lowest sinusoid frequency (sin(1e-4 t) ~ 1e-4 t, module_util.py:36-48); prompt_mlp and
+        every ResBlock mlp read none of them, except the scale rows of final_res_block channels
+        0..5 (weights w_g1, fitted to g1 - 1 at t = 1..T) and 6..11 (w_g2, to g2 - 1);
+      * final_res_block.block1 channel pairs (2j, 2j+1) = +-(x - mu)_j, (6+2j, 7+2j) = +-D_j;
+        block2 re-forms the pairs and final_conv takes differences: SiLU(z) - SiLU(-z) = z
+        exactly, so neither nonlinearity distorts the path;
+      * final_res_block.res_conv rows 0..11, final_conv columns 12..63 and its bias are zero.
+    `w_g1`, `w_g2` (length T) and `k` are fitted by the fixture generator on the reference and
+    stored in the fixture. Returns a new {key: float32 array}."""
+    sd = {key: np.array(v, np.float32, copy=True) for key, v in sd.items()}
+    T, kd = TRACK_T, TRACK_KNOTS
+    other = np.setdiff1d(np.arange(256), kd)
+    w1 = sd["time_mlp.1.weight"]
+    w1[kd] = 0.0
+    w1[kd, 31] = -TRACK_GAMMA * 1e4
+    sd["time_mlp.1.bias"][kd] = TRACK_GAMMA * (np.arange(T) + 1.5)
+    w3 = sd["time_mlp.3.weight"]
+    w3[kd] = 0.0
+    w3[kd, kd] = 1.0
+    w3[np.ix_(other, kd)] = 0.0
+    sd["time_mlp.3.bias"][kd] = 0.0
+    sd["prompt_mlp.weight"][kd] = 0.0
+    sd["prompt_mlp.bias"][kd] = 0.0
+    for key in sd:
+        if key.endswith(".mlp.1.weight"):
+            sd[key][:, kd] = 0.0
+    ic = sd["init_conv.weight"]
+    ic[:3] = 0.0
+    p = "final_res_block."
+    c1, c2 = sd[p + "block1.proj.weight"], sd[p + "block2.proj.weight"]
+    c1[:12], c2[:12] = 0.0, 0.0
+    sd[p + "res_conv.weight"][:12] = 0.0
+    fc = sd["final_conv.weight"]
+    fc[:] = 0.0
+    sd["final_conv.bias"][:] = 0.0
+    A = synth_tensor("tracking.D", (3, 64, 3, 3), seed=0)
+    for j in range(3):
+        ic[j, j, 3, 3] = 1.0
+        c1[2 * j, 64 + j, 1, 1], c1[2 * j + 1, 64 + j, 1, 1] = 1.0, -1.0
+        c1[6 + 2 * j, :64], c1[7 + 2 * j, :64] = k * A[j], -k * A[j]
+        for q in (2 * j, 6 + 2 * j):
+            c2[q, q, 1, 1], c2[q, q + 1, 1, 1] = 1.0, -1.0
+            c2[q + 1, q, 1, 1], c2[q + 1, q + 1, 1, 1] = -1.0, 1.0
+        fc[j, 2 * j, 1, 1], fc[j, 2 * j + 1, 1, 1] = 1.0, -1.0
+        fc[j, 6 + 2 * j, 1, 1], fc[j, 7 + 2 * j, 1, 1] = -1.0, 1.0
+    mw, mb = sd[p + "mlp.1.weight"], sd[p + "mlp.1.bias"]
+    mw[:12], mb[:12] = 0.0, 0.0
+    mw[64:76], mb[64:76] = 0.0, 0.0                  # their shifts
+    for r in range(6):
+        mw[r, kd] = w_g1
+        mw[6 + r, kd] = w_g2
+    return sd

@@ -11,6 +11,7 @@
  *       (load_network) and networks.py:10-15 (define_G -> ConditionalUNet(**setting)).
  *   dac_encode_image
  *       replaces DaCLIP.encode_image(image, control=True)   (open_clip/daclip_model.py:46-53)
+ *       and, with degra_ctx NULL, encode_image(image, control=False) (daclip_model.py:54-55)
  *   dac_encode_text / dac_degradation_probs
  *       replace DaCLIP.encode_text (daclip_model.py:125-126 -> model.py:237-249) and the
  *       degradation-class scoring softmax(100 d^ t^T) -> argmax (evaluate_daclip.py:45-84)
@@ -94,7 +95,10 @@ int dac_set_weight(dac_handle* h, const char* key, const void* data, const int64
 /* Strict check: every key the configured networks need was set. */
 int dac_finalize_weights(dac_handle* h);
 
-/* img [B,3,S,S] (preprocessed, S = image_size) -> image_ctx [B,E], degra_ctx [B,E] fp32. */
+/* img [B,3,S,S] (preprocessed, S = image_size) -> image_ctx [B,E], degra_ctx [B,E] fp32.
+ * degra_ctx NULL runs DaCLIP.encode_image(image, control=False) instead
+ * (open_clip/daclip_model.py:54-55 -> CLIP.encode_image, model.py:233-235): the clip tower
+ * alone, no controller hiddens, its features in image_ctx. */
 int dac_encode_image(dac_handle* h, const float* img, int B, float* image_ctx,
                      float* degra_ctx, void* stream);
 

@@ -63,13 +63,17 @@ def vision_forward(sd, p, img, layers, heads, control_tower=False, control=None)
     return (pooled, hiddens) if control_tower else pooled
 
 
-def encode_image(sd, img, layers=None, heads=None):
-    """DaCLIP.encode_image(image, control=True) -> (image_features, degra_features)."""
+def encode_image(sd, img, layers=None, heads=None, control=True):
+    """DaCLIP.encode_image(image, control=True) -> (image_features, degra_features)
+    (daclip_model.py:46-53); control=False -> CLIP.encode_image (daclip_model.py:54-55,
+    model.py:233-235): the clip tower's features alone."""
     width = sd["clip.visual.class_embedding"].shape[0]
     heads = heads or width // 64
     if layers is None:
         layers = 1 + max(int(k.split(".")[4]) for k in sd
                          if k.startswith("clip.visual.transformer.resblocks."))
+    if not control:
+        return vision_forward(sd, "clip.visual.", img, layers, heads)
     degra, hiddens = vision_forward(sd, "visual_control.", img, layers, heads, control_tower=True)
     image = vision_forward(sd, "clip.visual.", img, layers, heads, control=hiddens)
     return image, degra

@@ -29,3 +29,20 @@ def golden():
 def unet_sd():
     from daclip_amd import arch, synth
     return synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), seed=0)
+
+
+@pytest.fixture(scope="session")
+def restore_fixture():
+    """tests/golden/restore_rain_256_t100.npz (make_golden.py gen_restore) with its UNet weights
+    (synth.tracking_state_dict over the seed-0 synthetic weights) and injected noises."""
+    import numpy as np
+    from daclip_amd import arch, synth
+    g = dict(np.load(os.path.join(GOLDEN, "restore_rain_256_t100.npz")))
+    base = synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), seed=0)
+    sd = synth.tracking_state_dict(base, g["w_g1"], g["w_g2"], float(g["k"]))
+    shape = (1, 3, 256, 256)
+    noise = dict(n0=synth.synth_noise(shape, seed=91, tag="rs_noise_state"),
+                 steps=synth.synth_noise((100,) + shape, seed=92, tag="rs_steps"),
+                 n0_64=synth.synth_noise((1, 3, 64, 64), seed=91, tag="sde64_noise_state"),
+                 steps_64=synth.synth_noise((100, 1, 3, 64, 64), seed=92, tag="sde64_steps"))
+    return g, sd, noise

@@ -178,6 +178,131 @@ def gen_headline():
                         lq_u8=lq_u8, psnr_out_vs_lq=np.float64(ref_utils.calculate_psnr(out_u8, lq_u8)))
 
 
+RESTORE_IMAGE = "/root/reference/images/3_rain.png"     # BASELINE configs[0]: the rainy sample
+RESTORE_T = synth.TRACK_T
+
+
+def restore_noise(shape_lq, T=RESTORE_T, tag="rs"):
+    """Injected noises of the restoration fixtures (regenerated by the tests, never stored)."""
+    n0 = synth.synth_noise(shape_lq, seed=91, tag=tag + "_noise_state")
+    steps = synth.synth_noise((T,) + tuple(shape_lq), seed=92, tag=tag + "_steps")
+    return n0, steps
+
+
+def rain_crop():
+    """256x256 centre crop of the rainy sample (720x480), uint8 RGB."""
+    from PIL import Image
+    im = np.asarray(Image.open(RESTORE_IMAGE).convert("RGB"))
+    h, w = im.shape[:2]
+    y, x = (h - 256) // 2, (w - 256) // 2
+    return np.ascontiguousarray(im[y:y + 256, x:x + 256])
+
+
+def fit_tracking(base, sde, features, deep_calib):
+    """Fits synth.tracking_state_dict's free parameters on the reference modules: the
+    final_res_block scale rows (exact triangular solve on the reference's own hinge features
+    SiLU(t_emb(t)), t = 1..T; the hinges decrease in t, so the sums carry no cancellation) and
+    k, which scales D to std 0.04 on the fixture image at t = 1."""
+    kd = synth.TRACK_KNOTS
+    z = np.zeros(len(kd), np.float32)
+    sd0 = synth.tracking_state_dict(base, z, z, 1.0)
+    F = features(sd0).astype(np.float64)[:, kd]
+    tt = np.arange(1, RESTORE_T + 1)
+    sbar = sde.sigma_bars.numpy()[tt].astype(np.float64)
+    ea = np.exp(sde.thetas_cumsum.numpy()[tt].astype(np.float64) * float(sde.dt))
+    g1, g2 = 1.0 / sbar, 1.0 / (sbar * ea)
+    w1 = np.linalg.solve(F, g1 - 1.0).astype(np.float32)
+    w2 = np.linalg.solve(F, g2 - 1.0).astype(np.float32)
+    A = synth.synth_tensor("tracking.D", (3, 64, 3, 3), seed=0).astype(np.float64)
+    xin = deep_calib(sd0)[:, :64].astype(np.float64)
+    D = torch.nn.functional.conv2d(T(xin), T(A), padding=1).numpy()
+    k = float(np.float32(0.04 / D.std()))
+    return synth.tracking_state_dict(base, w1, w2, k), dict(g1=g1, g2=g2, w1=w1, w2=w2, k=k)
+
+
+def gen_restore():
+    """A restoration fixture on which the PSNR bar means something: the
+    reference's predict.py:58-91 flow on the 256x256 centre crop of images/3_rain.png
+    (BASELINE configs[0]) with synth.tracking_state_dict UNet weights (seed-0 synthetic weights
+    plus the fitted scale rows w_g1 / w_g2 and k, stored in the fixture), seed-0 ViT-B/32 DaCLIP, injected
+    noise, T=100 posterior, fp32 CPU; plus a full T=100 reverse_sde run at 64x64 with the same
+    weights (sde_utils.py:261-277)."""
+    from daclip_amd.preprocess import clip_transform
+    rgb = rain_crop()
+    image = rgb / 255.0                                              # predict.py:64 (float64)
+    img4clip = clip_transform(image).unsqueeze(0).numpy()
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    ic, dc = d.encode_image(T(img4clip), control=True)
+    ic, dc = ic.float(), dc.float()
+    lq = torch.tensor(image, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0)   # predict.py:73-75
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    spec = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    base = synth.synth_state_dict(spec, 0)
+    sde = ref_utils.IRSDE(max_sigma=50, T=RESTORE_T, schedule="cosine", eps=0.005, device="cpu")
+
+    def set_sd(sd):
+        m.load_state_dict({k: T(v) for k, v in sd.items()}, strict=True)
+
+    def features(sd):
+        set_sd(sd)
+        return np.concatenate([torch.nn.functional.silu(m.time_mlp(torch.tensor([float(t)]))).numpy()
+                               for t in range(1, RESTORE_T + 1)])
+
+    def deep_calib(sd):
+        set_sd(sd)
+        grab = {}
+        hk = m.final_res_block.register_forward_hook(lambda mod, a, o: grab.update(x=a[0]))
+        xt = lq + 0.004 * torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=93, tag="calib"))
+        m(xt, lq, 1.0, text_context=dc, image_context=ic)
+        hk.remove()
+        return grab["x"].numpy()
+
+    sd, info = fit_tracking(base, sde, features, deep_calib)
+    set_sd(sd)
+    # the fitted scales as the reference computes them
+    ss = np.concatenate([m.final_res_block.mlp(m.time_mlp(torch.tensor([float(t)]))).numpy()
+                         for t in range(1, RESTORE_T + 1)])
+    fit1 = np.abs((ss[:, 0] + 1) / info["g1"] - 1).max()
+    fit2 = np.abs((ss[:, 6] + 1) / info["g2"] - 1).max()
+    print(f"fit rel err g1 {fit1:.2e} g2 {fit2:.2e} k {info['k']:.4g}", flush=True)
+    seen = {}
+
+    def model(x, mu, t, **kw):                 # records the state the last step starts from
+        if float(t) == 1.0:
+            seen[tuple(x.shape)] = x.clone().numpy()
+        return m(x, mu, t, **kw)
+    sde.set_model(model)
+    n0, steps = restore_noise(tuple(lq.shape))
+    with NoiseInjector([n0]):
+        noisy = sde.noise_state(lq)
+    sde.set_mu(lq)
+    with NoiseInjector(list(steps)):
+        out = sde.reverse_posterior(noisy, text_context=dc, image_context=ic).numpy()
+    out_u8 = ref_utils.tensor2img(T(out.copy()).squeeze())
+    lq_u8 = ref_utils.tensor2img(lq.squeeze())
+    inr = float(((out > 0) & (out < 1)).mean())
+    psnr = ref_utils.calculate_psnr(out_u8, lq_u8)
+    print(f"restore: in-range {inr:.4f} range [{out.min():.3f},{out.max():.3f}] psnr vs lq {psnr:.3f}",
+          flush=True)
+    # full-length reverse_sde at 64x64 (a crop of the same image), same weights and contexts
+    lq64 = lq[:, :, 96:160, 96:160].contiguous()
+    s0, ssteps = restore_noise(tuple(lq64.shape), tag="sde64")
+    sde.set_mu(lq64)
+    with NoiseInjector([s0]):
+        noisy64 = sde.noise_state(lq64)
+    with NoiseInjector(list(ssteps)):
+        out_sde = sde.reverse_sde(noisy64, text_context=dc, image_context=ic).numpy()
+    print(f"sde64: in-range {float(((out_sde > 0) & (out_sde < 1)).mean()):.4f} "
+          f"range [{out_sde.min():.3f},{out_sde.max():.3f}]", flush=True)
+    np.savez_compressed(os.path.join(HERE, "restore_rain_256_t100.npz"), rgb_u8=rgb, img4clip=img4clip,
+                        image_context=ic.numpy(), degra_context=dc.numpy(), out=out, out_u8=out_u8,
+                        lq_u8=lq_u8, psnr_out_vs_lq=np.float64(psnr), out_sde64=out_sde,
+                        fit_rel=np.float64(max(fit1, fit2)), w_g1=info["w1"], w_g2=info["w2"],
+                        k=np.float32(info["k"]), x_t1=seen[tuple(lq.shape)],
+                        x_t1_sde64=seen[tuple(lq64.shape)])
+
+
 def gen_variants():
     """Two sampler / context variants of the reference, 16x16 / 32x32:
     * sample_T != T: IRSDE(T=100, sample_T=50) -> 50-entry schedule and the model called at
@@ -243,6 +368,21 @@ def gen_daclip():
     ic, dc = d.encode_image(T(img), control=True)
     np.savez_compressed(os.path.join(HERE, "daclip_small_encode.npz"), img=img,
                         image_context=ic.numpy(), degra_context=dc.numpy())
+
+
+def gen_plain_encode():
+    """DaCLIP.encode_image(image) with the reference's default control=False
+    (daclip_model.py:54-55 -> CLIP.encode_image, model.py:233-235): the clip tower alone."""
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    img = synth.synth_noise((2, 3, 224, 224), seed=11, tag="img4clip")
+    out = dict(b32=d.encode_image(T(img)).numpy(), b32_norm=d.encode_image(T(img), normalize=True).numpy())
+    small_v = dict(image_size=64, layers=3, width=128, patch_size=32)
+    small_t = dict(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+    d = _daclip(small_v, small_t, 64)
+    img = synth.synth_noise((3, 3, 64, 64), seed=12, tag="img4clip_small")
+    out["small"] = d.encode_image(T(img)).numpy()
+    np.savez_compressed(os.path.join(HERE, "daclip_plain_encode.npz"), **out)
 
 
 DEGRADATIONS = ["motion-blurry", "hazy", "jpeg-compressed", "low-light", "noisy", "raindrop",
@@ -361,7 +501,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["spec", "unet", "sde", "daclip", "text", "wild", "modules", "img"]
     fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
                text=gen_text, wild=gen_wild, modules=gen_modules, img=gen_img_metrics,
-               headline=gen_headline, variants=gen_variants)
+               headline=gen_headline, variants=gen_variants, restore=gen_restore,
+               plain=gen_plain_encode)
     for w in which:
         print("generating", w, flush=True)
         fns[w]()

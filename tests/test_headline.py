@@ -5,8 +5,10 @@ weights and injected noise). The HIP path restores B=8 copies through the captur
 
 North-star bar: restored output within 1e-3 dB PSNR of the reference CPU path. The fixture
 has no ground truth, so PSNR is taken against the LQ input (as the reference's predict flow
-would be scored on an LQ-only image). With seeded random weights the restoration saturates
-(most pixels clamp to 0 or 255 in tensor2img), so the float output is compared as well.
+would be scored on an LQ-only image). With seeded random weights the reference's loop
+diverges (|out| up to 273, 99.3 % of the pixels clamp in tensor2img), so this fixture says
+little about the PSNR bar: that is held on the restoration fixture instead (test_restore.py).
+Here the float output is compared, and the error on the 0.7 % of pixels in (0, 1) is bounded.
 """
 import json
 import os
@@ -72,7 +74,7 @@ def restore(dtype, g, lq, n0, steps, unet_sd):
     return ic.cpu().numpy(), dc.cpu().numpy(), out.cpu().numpy()
 
 
-def check(name, g, ic, dc, out, ctx_tol, out_tol):
+def check(name, g, ic, dc, out, ctx_tol, out_tol, unsat_tol):
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     assert rel(ic[0], g["image_context"][0]) < ctx_tol
     assert rel(dc[0], g["degra_context"][0]) < ctx_tol
@@ -90,12 +92,14 @@ def check(name, g, ic, dc, out, ctx_tol, out_tol):
            unsat_max_abs=float(np.abs(out[0] - ref)[unsat].max()))
     assert abs(d_psnr) < 1e-3                           # north-star bar
     assert r < out_tol
+    # the bound on the pixels this saturated fixture leaves in (0, 1), absolute
+    assert float(np.abs(out[0] - ref)[unsat].max()) < unsat_tol
 
 
 def test_headline_fp32_matches_reference(headline, unet_sd):
     g, lq, n0, steps = headline
     ic, dc, out = restore("fp32", g, lq, n0, steps, unet_sd)
-    check("headline_fp32", g, ic, dc, out, ctx_tol=1e-4, out_tol=1e-3)
+    check("headline_fp32", g, ic, dc, out, ctx_tol=1e-4, out_tol=1e-3, unsat_tol=1e-2)
 
 
 def test_headline_bf16_matches_reference(headline, unet_sd):
@@ -105,7 +109,7 @@ def test_headline_bf16_matches_reference(headline, unet_sd):
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     g, lq, n0, steps = headline
     ic, dc, out = restore("bf16", g, lq, n0, steps, unet_sd)
-    check("headline_bf16", g, ic, dc, out, ctx_tol=2e-2, out_tol=8e-4)
+    check("headline_bf16", g, ic, dc, out, ctx_tol=2e-2, out_tol=8e-4, unsat_tol=0.25)
     assert calculate_psnr(tensor2img(torch.from_numpy(out[0])), g["out_u8"]) > 50.0
 
 

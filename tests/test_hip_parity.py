@@ -260,3 +260,22 @@ def test_sharded_loop_equals_unsharded(unets, dt):
     s.image_offset = 0
     other = s.reverse_posterior(x0[2:3], T=nT, text_context=tc[2:3], image_context=ic[2:3])
     assert not torch.equal(other, full[2:3])
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_plain_encode_image_matches_reference(golden, dt):
+    """encode_image(image) with the reference's default control=False (daclip_model.py:54-55
+    -> CLIP.encode_image, model.py:233-235): the clip tower alone, a single tensor."""
+    from daclip_amd import arch
+    from daclip_amd.open_clip import DaCLIP
+    g = golden("daclip_plain_encode.npz")
+    m = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=dt, with_text=False)
+    m.load_synthetic(seed=0)
+    img = T(golden("daclip_b32_encode.npz")["img"])
+    out = m.encode_image(img)
+    assert isinstance(out, torch.Tensor)
+    tol = 1e-4 if dt == "fp32" else 2e-2
+    assert rel(out.cpu().numpy(), g["b32"]) < tol
+    assert rel(m.encode_image(img, normalize=True).cpu().numpy(), g["b32_norm"]) < tol
+    ic, dc = m.encode_image(img, control=True)          # the control path is unaffected
+    assert rel(ic.cpu().numpy(), golden("daclip_b32_encode.npz")["image_context"]) < tol

@@ -138,3 +138,20 @@ def test_headline_encode_matches_reference(golden):
     ic, dc = OC.encode_image(synth.synth_state_dict(spec, seed=0), g["img4clip"])
     assert rel(ic, g["image_context"]) < 1e-4
     assert rel(dc, g["degra_context"]) < 1e-4
+
+
+@pytest.mark.parametrize("which", ["small", "b32"])
+def test_plain_encode_matches_reference(golden, which):
+    """encode_image(image) with the default control=False (daclip_model.py:54-55)."""
+    from daclip_amd import arch, synth
+    g = golden("daclip_plain_encode.npz")
+    if which == "small":
+        v = arch.VisionConfig(image_size=64, patch_size=32, width=128, layers=3, embed_dim=64)
+        t = arch.TextConfig(context_length=16, vocab_size=64, width=64, heads=2, layers=1)
+        img = synth.synth_noise((3, 3, 64, 64), seed=12, tag="img4clip_small")
+    else:
+        v, t = arch.VIT_B_32, arch.TEXT_B_32
+        img = golden("daclip_b32_encode.npz")["img"]
+    spec = {k: s for k, s in arch.daclip_state_spec(v, t).items() if k.startswith("clip.visual.")}
+    out = OC.encode_image(synth.synth_state_dict(spec, seed=0), img, control=False)
+    assert rel(out, g[which]) < 1e-4

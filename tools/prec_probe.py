@@ -1,9 +1,9 @@
-"""Precision probe (GPU): which part of the bf16 path moves the headline restore away from the
-reference? Restores the headline fixture (B=1, 256^2, T=100) with encoder / UNet dtype
-combinations and prints delta-PSNR vs the reference output, out max-rel error and PSNR of the
-uint8 outputs against the reference's.
-    python tools/prec_probe.py [combo ...]   combo = <enc dtype>/<unet dtype>, e.g. fp32/bf16
-"""
+"""Precision probe (GPU): which part of the bf16 path moves the restoration fixture
+(tests/golden/restore_rain_256_t100.npz) away from the reference? One configuration per
+process (the DAC_EMU_W / DAC_EMU_A role masks of engine.cpp are read once):
+    [DAC_EMU_W=mask] [DAC_EMU_A=mask] python tools/prec_probe.py <enc dtype> <unet dtype> [label]
+Prints one JSON line: dPSNR vs the reference on the LQ, uint8 mismatch, float error RMS on the
+in-range pixels, and the error's regression on the restoration D = ref - LQ (scale error)."""
 import json
 import os
 import sys
@@ -21,38 +21,38 @@ def main():
     from daclip_amd.unet import ConditionalUNet
     from daclip_amd.sde import IRSDE
     from daclip_amd.preprocess import tensor2img, calculate_psnr
-    combos = sys.argv[1:] or ["fp32/fp32", "bf16/fp32", "fp32/bf16", "bf16/bf16"]
-    g = np.load(os.path.join(ROOT, "tests", "golden", "headline_256_t100.npz"))
+    e, u = sys.argv[1], sys.argv[2]
+    label = sys.argv[3] if len(sys.argv) > 3 else f"{e}/{u}"
+    g = np.load(os.path.join(ROOT, "tests", "golden", "restore_rain_256_t100.npz"))
     dev = torch.device("cuda", 0)
     lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0).to(dev)
-    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=71, tag="hl_noise_state")).to(dev)
-    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=72, tag="hl_steps")).to(dev)
-    usd = synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), seed=0)
-    clips, unets = {}, {}
-    for c in combos:
-        e, u = c.split("/")
-        if e not in clips:
-            clips[e] = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=e, with_text=False)
-            clips[e].load_synthetic(seed=0)
-        if u not in unets:
-            unets[u] = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype=u)
-            unets[u].load_state_dict(usd)
-    ref = g["out"][0]
-    for c in combos:
-        e, u = c.split("/")
-        ic, dc = clips[e].encode_image(torch.from_numpy(g["img4clip"]).to(dev), control=True)
-        s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
-        s.set_model(unets[u])
-        s.set_mu(lq)
-        out = s.reverse_posterior(s.noise_state(lq, noise=ns), noises=zs, text_context=dc, image_context=ic)
-        o = out[0].cpu().numpy()
-        u8 = tensor2img(out[0])
-        print(json.dumps({"combo": c,
-                          "delta_db": calculate_psnr(u8, g["lq_u8"]) - calculate_psnr(g["out_u8"], g["lq_u8"]),
-                          "psnr_vs_ref_u8": calculate_psnr(u8, g["out_u8"]),
-                          "out_rel": float(np.abs(o - ref).max() / np.abs(ref).max()),
-                          "out_rms_rel": float(np.sqrt(np.mean((o - ref) ** 2)) / np.sqrt(np.mean(ref ** 2)))}),
-              flush=True)
+    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=91, tag="rs_noise_state")).to(dev)
+    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=92, tag="rs_steps")).to(dev)
+    sd = synth.tracking_state_dict(synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), 0),
+                                   g["w_g1"], g["w_g2"], float(g["k"]))
+    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=e, with_text=False)
+    clip.load_synthetic(seed=0)
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype=u)
+    unet.load_state_dict(sd)
+    ic, dc = clip.encode_image(torch.from_numpy(g["img4clip"]).to(dev), control=True)
+    s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+    s.set_model(unet)
+    s.set_mu(lq)
+    out = s.reverse_posterior(s.noise_state(lq, noise=ns), noises=zs, text_context=dc, image_context=ic)
+    o = out[0].cpu().numpy().astype(np.float64)
+    ref = g["out"][0].astype(np.float64)
+    u8 = tensor2img(out[0])
+    err = o - ref
+    D = ref - lq[0].cpu().numpy()
+    inr = (ref > 0) & (ref < 1)
+    if os.environ.get("PROBE_SAVE"):
+        np.save(os.path.join(ROOT, "gpurun_out", f"probe_{label.replace('/', '_')}.npy"), o.astype(np.float32))
+    print(json.dumps({"label": label, "emu_w": os.environ.get("DAC_EMU_W"), "emu_a": os.environ.get("DAC_EMU_A"),
+                      "delta_db": float(calculate_psnr(u8, g["lq_u8"]) - calculate_psnr(g["out_u8"], g["lq_u8"])),
+                      "u8_mismatch": float(np.mean(u8 != g["out_u8"])),
+                      "err_rms": float(np.sqrt(np.mean(err[inr] ** 2))),
+                      "scale_err": float((err * D).sum() / (D * D).sum()),
+                      "corr": float(np.corrcoef(err.ravel(), D.ravel())[0, 1])}), flush=True)
 
 
 if __name__ == "__main__":
