@@ -22,7 +22,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "restored images/sec @256x256, 100 IR-SDE steps; PSNR vs ref; 1/2/4/8 MI355X"
-MFMA_PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # dense TFLOP/s (MI355X_MICROARCH.md)
+MFMA_PEAK = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
@@ -71,9 +71,14 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="images per GPU (8; wild-ir 2)")
     p.add_argument("--res", type=int, default=None, help="resolution (256; wild-ir 512)")
     p.add_argument("--T", type=int, default=100)
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
-                   help="bf16 (default); fp8 = e4m3 MX GEMMs for every conv/linear with Cin %% 64 == 0 "
-                        "(BASELINE configs[4]); fp32 = parity mode")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32", "fp8"],
+                   help="bf16 (default, BASELINE configs[1]); fp16 = IEEE half storage on the f16 MFMA "
+                        "(same bytes and rate, 8x finer rounding: the mode that holds the PSNR bar); "
+                        "fp8 = e4m3 MX GEMMs for every conv/linear with Cin %% 64 == 0 (BASELINE "
+                        "configs[4]); fp32 = parity mode")
+    p.add_argument("--modes", default="fp16",
+                   help="comma-separated extra dtypes measured after the main line on 1 GPU (throughput "
+                        "+ PSNR vs the reference), reported under 'modes'; 'none' to skip")
     p.add_argument("--kernel-id", type=int, default=312,
                    help="conv class timed for the roofline (kh*100 + variant; 312 = 3x3 interleaved-row v4 tiles)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -221,6 +226,43 @@ def psnr_sample(args, wu_keys, clip, unet_bf16, lq, img, dev):
                       f"({time.perf_counter() - t0:.1f}s)"}
 
 
+def extra_mode(args, dtype, dev, lq, img4clip, uspec, cspec):
+    """Another compute dtype on the same workload (1 GPU): its own handles, `warmup` + `steps`
+    timed restores of the same batch, and its PSNR against the reference fixture."""
+    from daclip_amd import synth
+    from daclip_amd.unet import ConditionalUNet
+    from daclip_amd.open_clip import DaCLIP
+    from daclip_amd.sde import IRSDE
+    ucfg, ukw, vcfg, tcfg = model_setup(args)
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], **ukw, device=dev, dtype=dtype)
+    unet.load_state_dict(synth.synth_state_dict(uspec, 0))
+    clip = DaCLIP(vcfg, tcfg, device=dev, dtype=dtype, with_text=False)
+    clip.load_state_dict(synth.synth_state_dict(cspec, 0), strict=False)
+    sde = IRSDE(max_sigma=50, T=args.T, schedule="cosine", eps=0.005)
+    sde.set_model(unet)
+    sde.set_mu(lq)
+
+    def step():
+        ic, dc = clip.encode_image(img4clip, control=True)
+        return sde.reverse_posterior(sde.noise_state(lq), text_context=dc, image_context=ic)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    B = lq.shape[0]
+    res = {"dtype": dtype, "value": round(B * args.steps / el, 4), "unit": "images/s",
+           "ms_per_step": round(el / args.steps * 1e3, 2), "outputs_finite": bool(torch.isfinite(out).all().item())}
+    if args.model == "universal-ir" and args.T == 100 and not args.no_psnr:
+        a2 = argparse.Namespace(**vars(args))
+        a2.dtype = dtype
+        res["psnr"] = psnr_vs_reference(a2, clip, dev)
+    return res
+
+
 def main():
     args = parse()
     ws, rank, local = setup_dist(args)
@@ -358,6 +400,9 @@ def main():
                "whole_path_tflops": round(total_tf * images / el, 1),
                "roofline": roof, "outputs_finite": finite, "psnr": psnr,
                "build": _lib.build_info()}
+        modes = [m for m in args.modes.split(",") if m and m != "none" and m != args.dtype]
+        if ws == 1 and modes:
+            res["modes"] = [extra_mode(args, m, dev, lq, img4clip, uspec, cspec) for m in modes]
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, synth.synth_state_dict(uspec, 0),
                                                synth.synth_state_dict(cspec, 0))

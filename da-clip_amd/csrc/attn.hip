@@ -12,6 +12,8 @@
 // small_mha: nn.MultiheadAttention core of the ViT blocks (transformer.py:203, 217-230):
 // L = 50 (B/32) tokens, 12 heads x 64; tiny, one workgroup per (image, head), fp32 math.
 #include "common.h"
+
+#include <atomic>
 #include "kernels.h"
 #include <cstdlib>
 
@@ -161,11 +163,11 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
       if constexpr (sizeof(T) == 2) {
 #pragma unroll
         for (int st = 0; st < 2; ++st) {           // k-step = 32 keys = subtiles 2st, 2st+1
-          bf16x8 pb;
+          typename Vec8<T>::t pb;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            pb[j] = (bf16)s[2 * st][j];
-            pb[4 + j] = (bf16)s[2 * st + 1][j];
+            pb[j] = (T)s[2 * st][j];
+            pb[4 + j] = (T)s[2 * st + 1][j];
           }
           const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
 #pragma unroll
@@ -203,7 +205,7 @@ __global__ void __launch_bounds__(256) flash_d32_kernel(const T* __restrict__ qk
 }
 
 // ------------------------------------------------------------------ K/V-resident variant
-// flash_kv_kernel (bf16, L % 128 == 0, L <= 1024 — the UNet's 32x32 SpatialTransformer levels
+// flash_kv_kernel (bf16 / f16, L % 128 == 0, L <= 1024 — the UNet's 32x32 SpatialTransformer levels
 // at 256^2): a block owns QG*128 queries of one (image, head) with 8 waves and keeps the head's
 // WHOLE K and V in LDS (L x 64 B each, 128 KB at L = 1024):
 //  * every K/V byte is DMA'd (global_load_lds, issued all at once in the prologue, 128-key
@@ -231,8 +233,8 @@ template <int N> DEV void fkv_wait(int n) {
   }
 }
 
-template <int QG>
-__global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __restrict__ qkv, bf16* o, int L,
+template <typename T, int QG>
+__global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restrict__ qkv, T* o, int L,
                                                               int H, float scale) {
   constexpr int D = 32;
   extern __shared__ __attribute__((aligned(1024))) char fkv_smem[];
@@ -246,7 +248,7 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
   const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + id / 8;
   const int bx = t % gx, h = (t / gx) % gy, b = t / (gx * gy);
   const int ld = 3 * H * D;
-  const bf16* base = qkv + (size_t)b * L * ld;
+  const T* base = qkv + (size_t)b * L * ld;
 
   // Q fragments first (their loads retire before the K/V DMAs in vmcnt order).
   u32x4 qf[QG];
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
     for (int c = 0; c < NC; ++c) {
       const int nn = 8 * c + wave;
       const int key = 16 * nn + kl;
-      const bf16* src = base + (size_t)key * ld + h * D + 8 * (ch ^ fkv_swz(key));
+      const T* src = base + (size_t)key * ld + h * D + 8 * (ch ^ fkv_swz(key));
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + H * D),
                                        (__attribute__((address_space(3))) void*)(sK + nn * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * H * D),
@@ -321,7 +323,7 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         s[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
-        Mma<bf16>::run(s[mi], kf[mi], qf[g]);
+        Mma<T>::run(s[mi], kf[mi], qf[g]);
       }
       float tmax = s[0][0];
 #pragma unroll
@@ -351,15 +353,15 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
       mrun[g] = mnew;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        bf16x8 pb;
+        typename Vec8<T>::t pb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          pb[j] = (bf16)s[2 * st][j];
-          pb[4 + j] = (bf16)s[2 * st + 1][j];
+          pb[j] = (T)s[2 * st][j];
+          pb[4 + j] = (T)s[2 * st + 1][j];
         }
         const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
 #pragma unroll
-        for (int dm = 0; dm < 2; ++dm) Mma<bf16>::run(oacc[g][dm], vf[st][dm], pbu);
+        for (int dm = 0; dm < 2; ++dm) Mma<T>::run(oacc[g][dm], vf[st][dm], pbu);
       }
     }
   }
@@ -369,12 +371,12 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
     l = red16_sum(l);
     l = red32_sum(l);
     const float inv = 1.f / l;
-    bf16* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
+    T* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
 #pragma unroll
     for (int dm = 0; dm < 2; ++dm) {
-      bf16x2_t v0, v1;
-      v0[0] = (bf16)(oacc[g][dm][0] * inv); v0[1] = (bf16)(oacc[g][dm][1] * inv);
-      v1[0] = (bf16)(oacc[g][dm][2] * inv); v1[1] = (bf16)(oacc[g][dm][3] * inv);
+      typename Vec8<T>::t2 v0, v1;
+      v0[0] = (T)(oacc[g][dm][0] * inv); v0[1] = (T)(oacc[g][dm][1] * inv);
+      v1[0] = (T)(oacc[g][dm][2] * inv); v1[1] = (T)(oacc[g][dm][3] * inv);
       uint2 st;
       st.x = __builtin_bit_cast(uint32_t, v0);
       st.y = __builtin_bit_cast(uint32_t, v1);
@@ -383,29 +385,40 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const bf16* __res
   }
 }
 
+template <typename T, int QG>
+static void fkv_optin() {
+  // > 64 KB of dynamic LDS must be opted into, once per (kernel, device).
+  static std::atomic<uint64_t> done{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev >= 64) dev = 63;
+  const uint64_t bit = 1ull << dev;
+  if (done.load(std::memory_order_acquire) & bit) return;
+  (void)hipFuncSetAttribute((const void*)flash_kv_kernel<T, QG>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+  done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
+// variant: 0 = the dispatcher's choice (g_flash_old = DAC_FLASH_OLD selects the staged-tile
+// kernel process-wide), 1 = the staged-tile kernel. Passed explicitly by the op-level test
+// hook, so no global state is toggled per call.
 template <typename T>
-void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
+void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale, int variant, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    if (L % 128 == 0 && L <= 1024 && !g_flash_old) {
+    if (L % 128 == 0 && L <= 1024 && variant == 0 && !g_flash_old) {
       // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
       // fills the chip, else 2 (or 1).
       const size_t smem = (size_t)L * 128;
-      static bool attr = false;
-      if (!attr) {                               // > 64 KB of dynamic LDS must be opted into
-        attr = true;
-        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-        (void)hipFuncSetAttribute((const void*)flash_kv_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-      }
       if (L % 512 == 0 && (long)(L / 512) * H * B >= 256) {
+        fkv_optin<T, 4>();
         dim3 g(L / 512, H, B);
-        flash_kv_kernel<4><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+        flash_kv_kernel<T, 4><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
       } else if (L % 256 == 0) {
+        fkv_optin<T, 2>();
         dim3 g(L / 256, H, B);
-        flash_kv_kernel<2><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+        flash_kv_kernel<T, 2><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
       } else {
+        fkv_optin<T, 1>();
         dim3 g(L / 128, H, B);
-        flash_kv_kernel<1><<<g, 64 * FKV_NW, smem, st>>>((const bf16*)qkv, (bf16*)o, L, H, scale);
+        flash_kv_kernel<T, 1><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
       }
       return;
     }
@@ -486,11 +499,18 @@ void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal,
   else __builtin_trap();
 }
 
+template <typename T>
+void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
+  flash_attn_d32_v<T>(qkv, o, B, L, H, scale, 0, st);
+}
+
 #define INST(T)                                                                           \
   template void flash_attn_d32<T>(const void*, void*, int, int, int, float, hipStream_t); \
+  template void flash_attn_d32_v<T>(const void*, void*, int, int, int, float, int, hipStream_t); \
   template void small_mha<T>(const void*, void*, int, int, int, int, int, hipStream_t);
 INST(float)
 INST(bf16)
+INST(f16)
 #undef INST
 
 }  // namespace dac

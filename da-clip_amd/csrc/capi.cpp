@@ -280,15 +280,14 @@ double dac_encode_flops(dac_handle* h, int B) {
 
 int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype, int variant,
                      void* stream) {
-  if (!qkv || !out || B <= 0 || L <= 0 || H <= 0 || (dtype != DAC_F32 && dtype != DAC_BF16) ||
-      variant < 0 || variant > 1)
+  if (!qkv || !out || B <= 0 || L <= 0 || H <= 0 ||
+      (dtype != DAC_F32 && dtype != DAC_BF16 && dtype != DAC_F16) || variant < 0 || variant > 1)
     return DAC_E_ARG;
-  const int keep = dac::g_flash_old;
-  dac::g_flash_old = variant == 1 ? 1 : keep;
   const float scale = 1.f / std::sqrt(32.f);
-  if (dtype == DAC_BF16) dac::flash_attn_d32<__bf16>(qkv, out, B, L, H, scale, (hipStream_t)stream);
-  else dac::flash_attn_d32<float>(qkv, out, B, L, H, scale, (hipStream_t)stream);
-  dac::g_flash_old = keep;
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == DAC_BF16) dac::flash_attn_d32_v<__bf16>(qkv, out, B, L, H, scale, variant, st);
+  else if (dtype == DAC_F16) dac::flash_attn_d32_v<_Float16>(qkv, out, B, L, H, scale, variant, st);
+  else dac::flash_attn_d32_v<float>(qkv, out, B, L, H, scale, variant, st);
   return hipGetLastError() == hipSuccess ? DAC_OK : DAC_E_HIP;
 }
 

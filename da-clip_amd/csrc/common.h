@@ -1,30 +1,56 @@
 // common.h — shared device helpers for the gfx950 kernels of libdaclip_hip.
 //
-// Storage/compute types: `float` (parity mode, exact-f32 MFMA v_mfma_f32_16x16x4_f32) and
-// `bf16` (perf mode, v_mfma_f32_16x16x32_bf16, fp32 accumulate). Every tile operand is
-// read from LDS as one 16-byte vector per lane, so one kernel body serves both types:
-// a 16-byte vector holds VE = 16/sizeof(T) elements (8 bf16 or 4 f32).
+// Storage/compute types: `float` (parity mode, exact-f32 MFMA v_mfma_f32_16x16x4_f32),
+// `bf16` (perf mode, v_mfma_f32_16x16x32_bf16, fp32 accumulate) and `f16` (IEEE half, same
+// shapes on v_mfma_f32_16x16x32_f16). Every tile operand is read from LDS as one 16-byte
+// vector per lane, so one kernel body serves all types: a 16-byte vector holds
+// VE = 16/sizeof(T) elements (8 bf16 / f16 or 4 f32).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef __bf16 bf16;
+typedef _Float16 f16;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define DEV __device__ __forceinline__
 
+// 16-bit storage types: bf16 (8-bit significand, the configs[1] perf mode) and IEEE fp16
+// (11-bit significand: 8x less rounding error at the same bytes and the same MFMA rate; the
+// mode that holds the 1e-3 dB PSNR bar). Both use 8 elements per 16-byte vector.
 template <typename T> struct TypeInfo;
 template <> struct TypeInfo<float> { static constexpr int VE = 4; };
 template <> struct TypeInfo<bf16> { static constexpr int VE = 8; };
+template <> struct TypeInfo<f16> { static constexpr int VE = 8; };
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> { typedef bf16x8 t; typedef bf16x2_t t2; };
+template <> struct Vec8<f16> { typedef f16x8 t; typedef f16x2_t t2; };
 
 DEV float to_f(float v) { return v; }
 DEV float to_f(bf16 v) { return (float)v; }
+DEV float to_f(f16 v) { return (float)v; }
 template <typename T> DEV T from_f(float v);
 template <> DEV float from_f<float>(float v) { return v; }
 template <> DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+template <> DEV f16 from_f<f16>(float v) { return (f16)v; }
+
+// Two packed 16-bit elements (low half first) -> two floats. bf16 by bit shifts (no
+// conversion instruction, no spills), fp16 by v_cvt_f32_f16.
+template <typename T> DEV void unpack2(unsigned u, float& lo, float& hi);
+template <> DEV void unpack2<bf16>(unsigned u, float& lo, float& hi) {
+  lo = __uint_as_float(u << 16);
+  hi = __uint_as_float(u & 0xffff0000u);
+}
+template <> DEV void unpack2<f16>(unsigned u, float& lo, float& hi) {
+  const f16x2_t h = __builtin_bit_cast(f16x2_t, u);
+  lo = (float)h[0];
+  hi = (float)h[1];
+}
 
 // Load / store VE elements (16 bytes) as fp32 values.
 template <typename T> DEV void load_vec(const T* p, float* out);
@@ -37,6 +63,11 @@ template <> DEV void load_vec<bf16>(const bf16* p, float* out) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) out[i] = (float)v[i];
 }
+template <> DEV void load_vec<f16>(const f16* p, float* out) {
+  f16x8 v = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = (float)v[i];
+}
 template <typename T> DEV void store_vec(T* p, const float* in);
 template <> DEV void store_vec<float>(float* p, const float* in) {
   *reinterpret_cast<f32x4*>(p) = f32x4{in[0], in[1], in[2], in[3]};
@@ -46,6 +77,12 @@ template <> DEV void store_vec<bf16>(bf16* p, const float* in) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) v[i] = (bf16)in[i];
   *reinterpret_cast<bf16x8*>(p) = v;
+}
+template <> DEV void store_vec<f16>(f16* p, const float* in) {
+  f16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (f16)in[i];
+  *reinterpret_cast<f16x8*>(p) = v;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -62,6 +99,13 @@ template <> struct Mma<bf16> {
   DEV static void run(f32x4& acc, const u32x4& a, const u32x4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<f16> {
+  static constexpr int KSTEP = 32;
+  DEV static void run(f32x4& acc, const u32x4& a, const u32x4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                 __builtin_bit_cast(f16x8, b), acc, 0, 0, 0);
   }
 };
 template <> struct Mma<float> {

@@ -107,5 +107,6 @@ void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {
 
 template void conv<float>(const ConvArgs&, int, int, int, int, hipStream_t);
 template void conv<bf16>(const ConvArgs&, int, int, int, int, hipStream_t);
+template void conv<f16>(const ConvArgs&, int, int, int, int, hipStream_t);
 
 }  // namespace dac

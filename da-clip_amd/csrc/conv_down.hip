@@ -1,4 +1,4 @@
-// conv_down.hip — the UNet's Downsample convs for bf16 handles: 4x4, stride 2, pad 1
+// conv_down.hip — the UNet's Downsample convs for 16-bit (bf16 / f16) handles: 4x4, stride 2, pad 1
 // (module_util.py:107-108 `nn.Conv2d(dim, dim_out, 4, 2, 1)`), Cin % 32 == 0, Cout % 64 == 0.
 //
 // The generic implicit GEMM gathered one input pixel per (output pixel, tap): 16 taps x 128 B
@@ -35,6 +35,7 @@ bool conv_down_ok(const ConvArgs& a) {
          (a.Ho * a.Wo) % CD_PIX == 0 && epi;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_down_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * CD_STAGE];
@@ -70,13 +71,13 @@ conv_down_kernel(ConvArgs a) {
     a_sl[k] = SB::slot(R, lane & 3) * 16;
   }
   // B DMA: row = kw * 64 + rho (rho = MFMA row, output channel n0 + wperm64(rho)).
-  const bf16* b_src[CD_NB / 4];
+  const T* b_src[CD_NB / 4];
   int b_sl[CD_NB / 4];
 #pragma unroll
   for (int k = 0; k < CD_NB / 4; ++k) {
     const int row = (wave + 4 * k) * 16 + (lane >> 2);
     const int kw = row >> 6, n = n0 + wperm64(row & 63);
-    b_src[k] = reinterpret_cast<const bf16*>(a.w) + (size_t)n * a.K + kw * a.Cin;
+    b_src[k] = reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + kw * a.Cin;
     b_sl[k] = SB::slot(row, lane & 3) * 8;
   }
   auto issue = [&](int c, int kh, int buf) {
@@ -142,7 +143,7 @@ conv_down_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[j], fa[i]);
+        for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], fw[j], fa[i]);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -151,12 +152,16 @@ conv_down_kernel(ConvArgs a) {
 #pragma unroll
   for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
   // Pixel tile i, lane lr: output pixel m0 + 32 * wave + 16 i + lr (tiles never straddle images).
-  epi_regs16<2>(a, acc, bi, nb, b, [&](int i) { return (size_t)(m0 + 32 * wave + 16 * i + lr); });
+  epi_regs16<T, 2>(a, acc, bi, nb, b, [&](int i) { return (size_t)(m0 + 32 * wave + 16 * i + lr); });
 }
 
+template <typename T>
 void conv_down(const ConvArgs& a, hipStream_t st) {
   const int npix = (int)((long)a.B * a.Ho * a.Wo / CD_PIX);
-  conv_down_kernel<<<dim3(npix, a.Cout / 64, 1), 256, 0, st>>>(a);
+  conv_down_kernel<T><<<dim3(npix, a.Cout / 64, 1), 256, 0, st>>>(a);
 }
+
+template void conv_down<bf16>(const ConvArgs&, hipStream_t);
+template void conv_down<f16>(const ConvArgs&, hipStream_t);
 
 }  // namespace dac

@@ -1,4 +1,4 @@
-// conv_edge.hip — the two edge convs of the ConditionalUNet for bf16 handles, each a
+// conv_edge.hip — the two edge convs of the ConditionalUNet for 16-bit (bf16 / f16) handles, each a
 // dedicated kernel because the generic implicit GEMM wastes most of its work on them:
 // (1) init_conv (conv7_kernel) and (2) final_conv (conv3n_kernel, below).
 //
@@ -24,7 +24,7 @@
 //    one barrier per tile.
 //  * Epilogue from registers: lane (r, g) of pixel tile t holds channels 16w + 4g .. +3 of
 //    pixel 16t + r: one 8-byte store, bias (if any) added in fp32.
-// MFMA: 16x16x32 bf16, A = weights (rows = output channels), B = pixels; hi and lo parts
+// MFMA: 16x16x32 bf16 / f16, A = weights (rows = output channels), B = pixels; hi and lo parts
 // accumulate into the same fp32 accumulator (= W.x with ~2^-17 weight error).
 #include "common.h"
 #include "kernels.h"
@@ -47,7 +47,7 @@ bool conv7_ok(const ConvArgs& a) {
          !a.ln_g && a.ldy % 4 == 0 && a.Ho == a.Hs && a.Wo == a.Ws;
 }
 
-template <int NP>
+template <typename T, int NP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv7_kernel(ConvArgs a, int ntiles) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * C7_BUF];
@@ -56,7 +56,7 @@ conv7_kernel(ConvArgs a, int ntiles) {
   const int nseg = (a.Wo + C7_SEG - 1) / C7_SEG;
 
   // Weight fragments (row-tap layout [o][part][kh][8 taps][8 ch], engine.cpp Packer::conv_dual).
-  const bf16* wg = reinterpret_cast<const bf16*>(a.w);
+  const T* wg = reinterpret_cast<const T*>(a.w);
   const int o = 16 * wave + lr;
   u32x4 wf[14][NP];
 #pragma unroll
@@ -105,7 +105,7 @@ conv7_kernel(ConvArgs a, int ntiles) {
     }
   };
 
-  bf16* y = reinterpret_cast<bf16*>(a.y);
+  T* y = reinterpret_cast<T*>(a.y);
   int t = t0, buf = 0;
   if (t < hi_x) issue(t, 0);
   for (; t < hi_x; t += nbx, buf ^= 1) {
@@ -116,7 +116,7 @@ conv7_kernel(ConvArgs a, int ntiles) {
     const char* hb = smem + buf * C7_BUF;
     const int seg = t % nseg, row = t / nseg;
     const int ow0 = seg * C7_SEG;
-    bf16* yrow = y + (size_t)row * a.Wo * a.ldy + 16 * wave + 4 * lg;
+    T* yrow = y + (size_t)row * a.Wo * a.ldy + 16 * wave + 4 * lg;
 #pragma unroll
     for (int grp = 0; grp < 2; ++grp) {
       f32x4 acc[8];
@@ -129,16 +129,16 @@ conv7_kernel(ConvArgs a, int ntiles) {
         for (int q = 0; q < 8; ++q) {
           const u32x4 xf = *reinterpret_cast<const u32x4*>(rb + q * 256);
 #pragma unroll
-          for (int p = 0; p < NP; ++p) Mma<bf16>::run(acc[q], wf[c][p], xf);
+          for (int p = 0; p < NP; ++p) Mma<T>::run(acc[q], wf[c][p], xf);
         }
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int ow = ow0 + grp * 128 + q * 16 + lr;
         if (ow < a.Wo) {
-          bf16x2_t v0, v1;
-          v0[0] = (bf16)(acc[q][0] + bi[0]); v0[1] = (bf16)(acc[q][1] + bi[1]);
-          v1[0] = (bf16)(acc[q][2] + bi[2]); v1[1] = (bf16)(acc[q][3] + bi[3]);
+          typename Vec8<T>::t2 v0, v1;
+          v0[0] = (T)(acc[q][0] + bi[0]); v0[1] = (T)(acc[q][1] + bi[1]);
+          v1[0] = (T)(acc[q][2] + bi[2]); v1[1] = (T)(acc[q][3] + bi[3]);
           typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
           u32x2 st;
           st[0] = __builtin_bit_cast(uint32_t, v0);
@@ -151,6 +151,7 @@ conv7_kernel(ConvArgs a, int ntiles) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+template <typename T>
 void conv7(const ConvArgs& a, hipStream_t st) {
   const int nseg = (a.Wo + C7_SEG - 1) / C7_SEG;
   const int ntiles = a.B * a.Ho * nseg;
@@ -164,8 +165,8 @@ void conv7(const ConvArgs& a, hipStream_t st) {
   if (G > ntiles) G = ntiles;
   if (G >= 8) G &= ~7;
   if (G < 1) return;
-  if (a.cwrap) conv7_kernel<2><<<G, 256, 0, st>>>(a, ntiles);
-  else conv7_kernel<1><<<G, 256, 0, st>>>(a, ntiles);
+  if (a.cwrap) conv7_kernel<T, 2><<<G, 256, 0, st>>>(a, ntiles);
+  else conv7_kernel<T, 1><<<G, 256, 0, st>>>(a, ntiles);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -202,7 +203,7 @@ bool conv3n_ok(const ConvArgs& a) {
          a.ldy >= a.Cout;
 }
 
-template <int NP>
+template <typename T, int NP>
 __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
   __shared__ __attribute__((aligned(1024))) char smem[CN_ST * CN_SLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -211,7 +212,7 @@ __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
 
   // A fragments: row lr = output channel (lr & 3) of part lr >> 2 (0 hi, 1 lo); rows past the
   // parts / channels are zero. Weight layout [o][tap][part][64] (engine.cpp Packer::conv_dual).
-  const bf16* wg = reinterpret_cast<const bf16*>(a.w);
+  const T* wg = reinterpret_cast<const T*>(a.w);
   const int o = lr & 3, part = lr >> 2;
   const bool live = o < a.Cout && part < NP;
   u32x4 wf[18];
@@ -257,7 +258,7 @@ __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
     }
   };
 
-  bf16* y = reinterpret_cast<bf16*>(a.y);
+  T* y = reinterpret_cast<T*>(a.y);
   constexpr int ND = CN_INSTR / 4;                // DMA instructions per wave per tile
   int t = t0;
 #pragma unroll
@@ -282,7 +283,7 @@ __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
       for (int q = 0; q < CN_R; ++q) {
         const int i = (q + kh) * CN_HP + 16 * wave + lr + kw;
         const u32x4 xf = *reinterpret_cast<const u32x4*>(hb + i * 128 + (((4 * h + lg) ^ (i & 7)) << 4));
-        Mma<bf16>::run(acc[q], wf[c], xf);
+        Mma<T>::run(acc[q], wf[c], xf);
       }
     }
     const int seg = t % nseg, rb = t / nseg;
@@ -302,12 +303,13 @@ __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
         if (lg == e) mine = ve;
       }
       const size_t m = ((size_t)rb * CN_R + q) * a.Wo + ow;     // (b*Ho + oh0 + q) * Wo + ow
-      if (lg < a.ldy) y[m * a.ldy + lg] = (bf16)(lg < a.Cout ? mine + bias : 0.f);
+      if (lg < a.ldy) y[m * a.ldy + lg] = (T)(lg < a.Cout ? mine + bias : 0.f);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+template <typename T>
 void conv3n(const ConvArgs& a, hipStream_t st) {
   const int ntiles = a.B * (a.Ho / CN_R) * (a.Wo / CN_SEG);
   static int ncu = 0;
@@ -320,8 +322,13 @@ void conv3n(const ConvArgs& a, hipStream_t st) {
   if (G > ntiles) G = ntiles;
   if (G >= 8) G &= ~7;
   if (G < 1) return;
-  if (a.Cin == 128) conv3n_kernel<2><<<G, 256, 0, st>>>(a, ntiles);
-  else conv3n_kernel<1><<<G, 256, 0, st>>>(a, ntiles);
+  if (a.Cin == 128) conv3n_kernel<T, 2><<<G, 256, 0, st>>>(a, ntiles);
+  else conv3n_kernel<T, 1><<<G, 256, 0, st>>>(a, ntiles);
 }
+
+template void conv7<bf16>(const ConvArgs&, hipStream_t);
+template void conv7<f16>(const ConvArgs&, hipStream_t);
+template void conv3n<bf16>(const ConvArgs&, hipStream_t);
+template void conv3n<f16>(const ConvArgs&, hipStream_t);
 
 }  // namespace dac

@@ -24,9 +24,10 @@ struct LinearRows {      // block-tile row t -> output row m0 + t
 
 template <typename T> DEV float silu_t(float x);
 template <> DEV float silu_t<float>(float x) { return x / (1.f + expf(-x)); }
-// bf16 outputs: v_rcp_f32 (1 ulp) instead of a correctly rounded reciprocal, which compiles
+// 16-bit outputs: v_rcp_f32 (1 ulp) instead of a correctly rounded reciprocal, which compiles
 // to the ~10-instruction IEEE division sequence and dominated the SiLU epilogues.
 template <> DEV float silu_t<bf16>(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+template <> DEV float silu_t<f16>(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 template <int BM, int BN>
 struct EpiLds {

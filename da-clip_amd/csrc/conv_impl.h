@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
 }
 
 
-// Register epilogue of the swapped-operand bf16 tiles (weights as the MFMA A operand, weight
+// Register epilogue of the swapped-operand 16-bit tiles (weights as the MFMA A operand, weight
 // row p holding output channel 16*((p>>2)&3) + 4*(p>>4) + (p&3) of its 64-channel tile):
 // acc[i][j][r] is channel nb + 4j + r of output row pix(i), nb = tile base + 16*(lane>>4), so
 // each lane finishes 16 consecutive channels with 16-byte loads and stores, no LDS staging.
@@ -213,13 +213,13 @@ template <int TM> struct EpiPref { u32x4 v[2 * TM > 8 ? 2 * TM : 8]; };
 DEV void ld_asm(u32x4& r, const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
 }
-template <int TM, class PixOf>
+template <typename T, int TM, class PixOf>
 DEV void epi_prefetch(const ConvArgs& a, int nb, int b, const PixOf& pix, EpiPref<TM>& p) {
   // One set of loads whatever the operand (addresses selected, not branches): per-branch
   // destinations would be merged by register copies, reading registers still in flight.
   constexpr int N = 2 * TM > 8 ? 2 * TM : 8;
   if (!a.res1 && !a.ss) return;
-  const bf16* r1 = reinterpret_cast<const bf16*>(a.res1);
+  const T* r1 = reinterpret_cast<const T*>(a.res1);
   const float* s4 = a.ss + (size_t)b * a.ss_ld + nb;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
@@ -232,10 +232,10 @@ DEV void epi_prefetch(const ConvArgs& a, int nb, int b, const PixOf& pix, EpiPre
 
 // PRE: operands come from epi_prefetch and the conv has no bbias / res2 / (ss with res1) —
 // the epilogue then issues no loads at all, so it never waits for in-flight DMA.
-template <int TM, bool LN = false, bool PRE = false, class PixOf>
+template <typename T, int TM, bool LN = false, bool PRE = false, class PixOf>
 DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
                     const PixOf& pix, const EpiPref<TM>* pre = nullptr, const float* ssl = nullptr) {
-  bf16* y = reinterpret_cast<bf16*>(a.y);
+  T* y = reinterpret_cast<T*>(a.y);
   __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
   if constexpr (PRE) {
     // Every prefetched register stays allocated until here (after the caller's wait), also the
@@ -279,7 +279,7 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
-      if (a.act == ACT_SILU) u = silu_t<bf16>(u);
+      if (a.act == ACT_SILU) u = silu_t<T>(u);
       v[e] = u;
     }
     if constexpr (LN) {
@@ -302,28 +302,30 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
     for (int h = 0; h < 2; ++h) {
       if (a.res1) {
         const u32x4 r1 = PRE ? pre->v[2 * i + h]
-                             : *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(a.res1) + m * a.ldr1 + nb + 8 * h);
+                             : *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res1) + m * a.ldr1 + nb + 8 * h);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {              // bf16 pair -> two floats by bit shifts (no spills)
-          const unsigned u = r1[w];
-          v[8 * h + 2 * w] += __uint_as_float(u << 16);
-          v[8 * h + 2 * w + 1] += __uint_as_float(u & 0xffff0000u);
+        for (int w = 0; w < 4; ++w) {              // element pair -> two floats (no spills)
+          float lo, hi;
+          unpack2<T>(r1[w], lo, hi);
+          v[8 * h + 2 * w] += lo;
+          v[8 * h + 2 * w + 1] += hi;
         }
       }
       if (!PRE && a.res2) {
-        const u32x4 r2 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16*>(a.res2) + m * a.ldr2 + nb + 8 * h);
+        const u32x4 r2 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res2) + m * a.ldr2 + nb + 8 * h);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
-          const unsigned u = r2[w];
-          v[8 * h + 2 * w] += __uint_as_float(u << 16);
-          v[8 * h + 2 * w + 1] += __uint_as_float(u & 0xffff0000u);
+          float lo, hi;
+          unpack2<T>(r2[w], lo, hi);
+          v[8 * h + 2 * w] += lo;
+          v[8 * h + 2 * w + 1] += hi;
         }
       }
       if (!PRE && a.bbias) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[8 * h + e] += bb[8 * h + e];
       }
-      store_vec<bf16>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
+      store_vec<T>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
     }
   }
 }
@@ -538,7 +540,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     float bi[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-    epi_regs16<TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+    epi_regs16<T, TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
   } else {
     conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
   }
@@ -1069,7 +1071,7 @@ conv3i_kernel(ConvArgs a, int RW) {
     if constexpr (SWAP && kh == 2) {
       if (s + 1 == S && pre_ok) {
         const int nb = n0 + wn * WTN + 16 * lg;
-        epi_prefetch<TM>(a, nb, b, pixf, pref);
+        epi_prefetch<T, TM>(a, nb, b, pixf, pref);
       }
     }
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
@@ -1103,19 +1105,19 @@ conv3i_kernel(ConvArgs a, int RW) {
     const float* el = reinterpret_cast<const float*>(smem + ST * STAGE) + 16 * lg;   // LDS terms
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = el[128 + e];
-    if (pre_ok) epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
-    else epi_regs16<TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
+    if (pre_ok) epi_regs16<T, TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
+    else epi_regs16<T, TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
     if constexpr (RES) {
       // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
-      bf16* y2 = reinterpret_cast<bf16*>(a.y2);
+      T* y2 = reinterpret_cast<T*>(a.y2);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const size_t m = (size_t)rm(wm * WTM + TM * lr + i);
         float v[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) v[e] = accR[i][e >> 2][e & 3] + (a.bias2 ? a.bias2[nb + e] : 0.f);
-        store_vec<bf16>(y2 + m * a.ldy2 + nb, v);
-        store_vec<bf16>(y2 + m * a.ldy2 + nb + 8, v + 8);
+        store_vec<T>(y2 + m * a.ldy2 + nb, v);
+        store_vec<T>(y2 + m * a.ldy2 + nb + 8, v + 8);
       }
     }
   } else {
@@ -1187,7 +1189,7 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
   }
 }
 
-// v5: weight-stationary 3x3 conv for Cin = Cout = 64 (bf16), the ResBlock convs of the
+// v5: weight-stationary 3x3 conv for Cin = Cout = 64 (16-bit types), the ResBlock convs of the
 // 256x256 / 128x128 levels, whose K = 576 is too short for v4's per-stage weight copies to
 // amortise. The block loads all 9 taps x 64 x 64 weights (72 KB) into LDS once and then
 // never synchronises again: each of its 8 waves owns a private 2-stage ring holding only its
@@ -1213,7 +1215,7 @@ struct C3W {
   static constexpr int SMEM = C3W_WBYTES + NWV * NST * STAGE;
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
-template <int NWV, int TM = 4, int NST = 2>
+template <typename T, int NWV, int TM = 4, int NST = 2>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
   using CF = C3W<NWV, TM, NST>;
   constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
@@ -1232,7 +1234,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
     const int c = g / 9, tap = g % 9;
     const int n = wperm64(rho);
     const int L = SB::slot(rho, lane & 3);
-    const bf16* src = reinterpret_cast<const bf16*>(a.w) + (size_t)n * a.K + tap * 64 + c * 32 + L * VE;
+    const T* src = reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + tap * 64 + c * 32 + L * VE;
     __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(smem + q * 1024), 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1325,7 +1327,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
       } else {
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((NST - 2) * NI) : "memory");
       }
-      if (s == 5) epi_prefetch<TM>(a, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, pref);
+      if (s == 5) epi_prefetch<T, TM>(a, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, pref);
       {
         const int sn = s + NST - 1;                   // stage to issue: (tile + sn/6, sn%6)
         issue(t + (sn / 6) * stride, (sn % 6) / 3, sn % 3, (slot + NST - 1) % NST);
@@ -1349,14 +1351,14 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) Mma<bf16>::run(acc[i][j], fw[kw & 1][j], fa[i + kw]);
+          for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], fw[kw & 1][j], fa[i + kw]);
       }
       slot = slot + 1 == NST ? 0 : slot + 1;
     }
     // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15. The
     // prefetched operands landed once at most the next tile's first stage (NI DMA) is pending.
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
-    epi_regs16<TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, &pref);
+    epi_regs16<T, TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, &pref);
     if (tn >= t_end) break;
     t = tn;
   }
@@ -1386,12 +1388,13 @@ inline int conv3w_blocks(int ntiles, int nwv) {
   if (nb > ncu) nb = ncu;
   return (nb + 7) / 8 * 8;                          // whole XCD bands
 }
-inline void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
+template <typename T>
+void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   const C3WCfg c = c3w_cfg();
 #define DAC_C3W(NW_, TM_, NS_)                                                                 \
   if (c.nwv == NW_ && c.tm == TM_ && c.nst == NS_ && a.Wo % (16 * TM_) == 0) {                  \
     const int ntiles = a.B * a.Ho * (a.Wo / (16 * TM_));                                        \
-    conv3w_kernel<NW_, TM_, NS_><<<conv3w_blocks(ntiles, NW_), 64 * NW_, 0, st>>>(a, ntiles, delay); \
+    conv3w_kernel<T, NW_, TM_, NS_><<<conv3w_blocks(ntiles, NW_), 64 * NW_, 0, st>>>(a, ntiles, delay); \
     return;                                                                                     \
   }
   DAC_C3W(8, 2, 3)
@@ -1401,7 +1404,7 @@ inline void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   DAC_C3W(6, 4, 2)
 #undef DAC_C3W
   const int ntiles = a.B * a.Ho * (a.Wo >> 6);
-  conv3w_kernel<C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+  conv3w_kernel<T, C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
 }
 
 template <typename T, int KH, int KW, int S, int P>
@@ -1419,7 +1422,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
   const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2) {
     if (g_conv3_force < 0 && conv3n_ok(a)) {   // final_conv: conv_edge.hip
-      conv3n(a, st);
+      conv3n<T>(a, st);
       return;
     }
   }
@@ -1431,22 +1434,22 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / (int)sizeof(T)) == 0)
       if (conv3i_try<T, 256, 16, 4, 1, 64, 2, 3, EPI_ALL>(a, st)) return;
   }
-  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && std::is_same<T, bf16>::value) {
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2) {
     if ((g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) {
       const int delay = g_conv3_force >= 30 ? (g_conv3_force - 30) * 2 : 6;   // swept: 4-10 best
-      conv3w_launch(a, delay, st);
+      conv3w_launch<T>(a, delay, st);
       return;
     }
   }
   if constexpr (KH == 4 && KW == 4 && S == 2 && P == 1 && sizeof(T) == 2) {
     if (g_conv3_force < 0 && conv_down_ok(a)) {
-      conv_down(a, st);
+      conv_down<T>(a, st);
       return;
     }
   }
   if constexpr (KH == 7 && KW == 7 && S == 1 && P == 3 && sizeof(T) == 2) {
     if (conv7_ok(a)) {
-      conv7(a, st);
+      conv7<T>(a, st);
       return;
     }
     if (a.Cin == 8 && a.K == (a.cwrap ? 2 : 1) * 7 * 8 * 8 && a.zero && a.amode == 0 && a.w_bstride == 0 && !a.x2) {

@@ -112,25 +112,70 @@ static float bf2f_host(uint16_t h) {
   std::memcpy(&f, &u, 4);
   return f;
 }
-// The bf16 neighbour of h one step toward f (h != f, both finite).
-static uint16_t bf_toward(uint16_t h, float f) {
-  const float v = bf2f_host(h);
+// Host f32 -> IEEE half, round to nearest even (subnormals kept, overflow to +-inf).
+static uint16_t f2h_host(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);          // >= 65520 -> inf
+  if (ax < 0x38800000u) {                                             // |f| < 2^-14: subnormal
+    float a;
+    std::memcpy(&a, &ax, 4);
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(a * 16777216.f));   // a * 2^24 is exact
+  }
+  uint32_t h = (((ax >> 23) - 112u) << 10) | ((ax & 0x7fffffu) >> 13);
+  const uint32_t rem = ax & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+static float h2f_host(uint16_t h) {
+  const int e = (h >> 10) & 0x1f;
+  const uint32_t m = h & 0x3ffu;
+  float v = e == 0 ? std::ldexp((float)m, -24)
+                   : e == 31 ? (m ? NAN : INFINITY) : std::ldexp((float)(m | 0x400u), e - 25);
+  return (h & 0x8000u) ? -v : v;
+}
+// 16-bit storage codecs of the packed weights (bf16 / IEEE half), round to nearest even.
+struct BF16Codec {
+  static constexpr bool kHalf = false;
+  static uint16_t enc(float f) { return f2bf_host(f); }
+  static float dec(uint16_t h) { return bf2f_host(h); }
+};
+struct F16Codec {
+  static constexpr bool kHalf = true;
+  static uint16_t enc(float f) { return f2h_host(f); }
+  static float dec(uint16_t h) { return h2f_host(h); }
+};
+template <typename T> struct CodecOf { typedef BF16Codec type; };
+template <> struct CodecOf<f16> { typedef F16Codec type; };
+// The 16-bit neighbour of h one step toward f (h != f, both finite); both formats are
+// sign-magnitude, so a magnitude step is +-1 on the bits.
+template <class C>
+static uint16_t step_toward(uint16_t h, float f) {
+  const float v = C::dec(h);
   const bool up = f > v;
   if (v == 0.f) return up ? 0x0001 : 0x8001;
   return (uint16_t)(((v > 0.f) == up) ? h + 1 : h - 1);
 }
-// Weight rounding to bf16. Round-to-nearest leaves a per-layer systematic error (the same
-// every step and pixel); by default (DAC_WROUND=1; 0 = plain RNE) each (output row, input channel) group of `taps`
-// kernel taps is rounded so that its sum is kept (greedy flips of the taps closest to the
-// rounding midpoint), which removes the error's response to smooth inputs.
+// Weight rounding to 16 bits. bf16 round-to-nearest leaves a per-layer systematic error (the
+// same every step and pixel); by default (DAC_WROUND=1) each bf16 (output row, input channel)
+// group of `taps` kernel taps is rounded so that its sum is kept (greedy flips of the taps
+// closest to the rounding midpoint), which removes the error's response to smooth inputs.
+// fp16 weights keep plain RNE: with an 11-bit significand the flips (up to 1 ulp per tap)
+// cost more texture-response accuracy than the DC error they remove (restoration fixture:
+// dPSNR -1.3e-3 dB with sum-keeping, -1.2e-4 dB with RNE). DAC_WROUND=0: RNE for both,
+// 2: sum-keeping for both.
 static int wround_mode() {
   static const int m = getenv("DAC_WROUND") ? env_mask("DAC_WROUND") : 1;   // default: sum-keeping
   return m;
 }
-static std::vector<uint16_t> quantize_bf16(const std::vector<float>& v, int taps, int cin) {
+template <class C>
+static std::vector<uint16_t> quantize16(const std::vector<float>& v, int taps, int cin) {
   std::vector<uint16_t> h(v.size());
-  for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf_host(v[i]);
-  if (wround_mode() != 1 || taps < 2) return h;
+  for (size_t i = 0; i < v.size(); ++i) h[i] = C::enc(v[i]);
+  const int m = wround_mode();
+  if (taps < 2 || m == 0 || (m == 1 && C::kHalf)) return h;
   const size_t rows = v.size() / ((size_t)taps * cin);
   std::vector<size_t> idx(taps);
   std::vector<char> used(taps);
@@ -140,7 +185,7 @@ static std::vector<uint16_t> quantize_bf16(const std::vector<float>& v, int taps
       for (int t = 0; t < taps; ++t) {
         idx[t] = (o * taps + t) * cin + c;
         used[t] = 0;
-        r += (double)v[idx[t]] - bf2f_host(h[idx[t]]);
+        r += (double)v[idx[t]] - C::dec(h[idx[t]]);
       }
       for (int it = 0; it < taps; ++it) {
         int best = -1;
@@ -148,13 +193,13 @@ static std::vector<uint16_t> quantize_bf16(const std::vector<float>& v, int taps
         for (int t = 0; t < taps; ++t) {
           const float w = v[idx[t]];
           const uint16_t q = h[idx[t]];
-          if (used[t] || bf2f_host(q) == w || !std::isfinite(w)) continue;
-          const double nr = r + (double)bf2f_host(q) - bf2f_host(bf_toward(q, w));
+          if (used[t] || C::dec(q) == w || !std::isfinite(w)) continue;
+          const double nr = r + (double)C::dec(q) - C::dec(step_toward<C>(q, w));
           if (std::fabs(nr) < br) { br = std::fabs(nr); best = t; }
         }
         if (best < 0) break;
-        const uint16_t q = h[idx[best]], q2 = bf_toward(q, v[idx[best]]);
-        r += (double)bf2f_host(q) - bf2f_host(q2);
+        const uint16_t q = h[idx[best]], q2 = step_toward<C>(q, v[idx[best]]);
+        r += (double)C::dec(q) - C::dec(q2);
         h[idx[best]] = q2;
         used[best] = 1;
       }
@@ -216,12 +261,20 @@ struct Packer {
     if (cin <= 1) cin = (int)v.size(), taps = 1;
     if (sizeof(T) == 4) {
       if (!emu_w_key(key)) return pool.upload(v.data(), v.size() * 4);
-      const std::vector<uint16_t> h = quantize_bf16(v, taps, cin);
       std::vector<float> q(v.size());
+      if (getenv("DAC_EMU_FP16") && atoi(getenv("DAC_EMU_FP16"))) {
+        for (size_t i = 0; i < v.size(); ++i) {        // round to 11 significant bits (normals)
+          int e;
+          const double m = std::frexp((double)v[i], &e);
+          q[i] = (float)std::ldexp(std::nearbyint(std::ldexp(m, 11)), e - 11);
+        }
+        return pool.upload(q.data(), q.size() * 4);
+      }
+      const std::vector<uint16_t> h = quantize16<BF16Codec>(v, taps, cin);
       for (size_t i = 0; i < v.size(); ++i) q[i] = bf2f_host(h[i]);
       return pool.upload(q.data(), q.size() * 4);
     }
-    const std::vector<uint16_t> h = quantize_bf16(v, taps, cin);
+    const std::vector<uint16_t> h = quantize16<typename CodecOf<T>::type>(v, taps, cin);
     return pool.upload(h.data(), h.size() * 2);
   }
   const float* f32(const std::string& key, std::vector<int64_t> shape) {
@@ -264,10 +317,10 @@ struct Packer {
   ConvW linear(const std::string& key, int O, int I, const std::string& bkey = "") {
     return conv(key, O, I, 1, 1, bkey, true);
   }
-  // Split-precision weights (bf16 handles; fp32 handles keep plain fp32 weights): hi = RNE(w),
+  // Split-precision weights (16-bit handles; fp32 handles keep plain fp32 weights): hi = RNE(w),
   // lo = RNE(w - hi), packed [O][kh][kws][hi cin | lo cin], or, for the 7x7 row-tap layout
   // (kwp > kw), [O][hi rows | lo rows]. The layer then computes A.hi + A.lo in one fp32
-  // accumulator: weight error ~2^-17 relative instead of bf16's 2^-9.
+  // accumulator: weight error ~2^-17 (bf16) / 2^-23 (f16) relative instead of 2^-9 / 2^-12.
   ConvW conv_dual(const std::string& key, int O, int C, int kh, int kw, const std::string& bkey = "",
                   int kwp = 0) {
     if (sizeof(T) == 4) return conv(key, O, C, kh, kw, bkey, false, kwp);
@@ -286,7 +339,8 @@ struct Packer {
         for (int y = 0; y < kh; ++y)
           for (int x = 0; x < kw; ++x) {
             const float v = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
-            const uint16_t hi = f2bf_host(v), lo = f2bf_host(v - bf2f_host(hi));
+            using C = typename CodecOf<T>::type;
+            const uint16_t hi = C::enc(v), lo = C::enc(v - C::dec(hi));
             const size_t tap = (size_t)y * kws + x;
             if (cw.kwp) {
               h[(size_t)o * 2 * per + tap * cw.cin + c] = hi;
@@ -769,12 +823,24 @@ struct UNetNet {
     T* weff = r.alloc<T>((size_t)B * C * 128);
     float* ws = r.alloc<float>(linear_attention_ws_floats(B, H * W));
     r.flops += 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32;
-    if (!r.dry) linear_attention_weff<T>(qkv, la.wout, weff, B, H * W, C, ws, r.st);
+    // f16: W_eff / HW is subnormal, so W_eff is stored times S / HW (S = 2^k >= HW) and the GEMM
+    // epilogue takes 1/S out exactly: (acc + 0) * (1 + (2^-k - 1)) + bout, from one shared
+    // scale/shift row (ss_ld = 0).
+    constexpr bool hw_late = std::is_same<T, f16>::value;
+    float* ssr = hw_late ? r.alloc<float>(2 * (size_t)C) : nullptr;
+    if (!r.dry) {
+      int k = 0;
+      while ((1 << k) < H * W) ++k;
+      const float S = std::ldexp(1.f, k);
+      linear_attention_weff<T>(qkv, la.wout, weff, B, H * W, C, ws, r.st, hw_late ? S / (float)(H * W) : 0.f);
+      if (hw_late) ss_fill(ssr, C, 1.f / S - 1.f, la.bout, r.st);
+    }
     ConvW wo;
-    wo.w = weff; wo.b = la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
+    wo.w = weff; wo.b = hw_late ? nullptr : la.bout; wo.cout = C; wo.cin = wo.cin_real = 128;
     T* t = r.alloc<T>(M * C);
     Epi eo;
     eo.amode = 1; eo.w_bstride = (long long)C * 128;
+    if (hw_late) { eo.ss = ssr; eo.ss_ld = 0; }
     conv_call<T>(r, wo, qkv, 384, 128, nullptr, 0, B, H, W, 0, 1, 0, t, C, eo);
     T* y = r.alloc<T>(M * C);
     ln<T>(r, t, C, y, C, x, C, la.gout, nullptr, (int)M, C, 1e-5f);
@@ -1454,12 +1520,15 @@ std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg
   if (dtype == DAC_F32) return std::make_unique<EngineT<float>>(device, cfg);
   if (dtype == DAC_BF16) return std::make_unique<EngineT<bf16>>(device, cfg);
   if (dtype == DAC_FP8) return std::make_unique<EngineT<bf16>>(device, cfg, true);
-  throw Error(DAC_E_ARG, "dtype must be DAC_F32, DAC_BF16 or DAC_FP8");
+  if (dtype == DAC_F16) return std::make_unique<EngineT<f16>>(device, cfg);
+  throw Error(DAC_E_ARG, "dtype must be DAC_F32, DAC_BF16, DAC_FP8 or DAC_F16");
 }
 
 template void conv_call<float>(Run&, const ConvW&, const void*, int, int, const void*, int, int,
                                int, int, int, int, int, void*, int, const Epi&);
 template void conv_call<bf16>(Run&, const ConvW&, const void*, int, int, const void*, int, int,
                               int, int, int, int, int, void*, int, const Epi&);
+template void conv_call<f16>(Run&, const ConvW&, const void*, int, int, const void*, int, int,
+                             int, int, int, int, int, void*, int, const Epi&);
 
 }  // namespace dac

@@ -1,6 +1,7 @@
 // kernels.h — host-side launchers of the gfx950 kernels (one .hip file per family).
 // All activations are NHWC ("rows" = pixels/tokens, row stride `ld` elements), stored as
-// T = float (parity mode) or bf16 (perf mode); small per-image vectors are fp32.
+// T = float (parity mode), bf16 (perf mode) or f16 (IEEE half perf mode); small per-image
+// vectors are fp32.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -57,7 +58,7 @@ struct ConvArgs {
 // The dispatcher can fuse a_w2/y2 into this 3x3 conv (bf16 v4 256x64 swapped-operand tiles).
 bool conv_res_fusable(const ConvArgs& a);
 
-// Shapes served by the weight-stationary 3x3 kernel (conv_impl.h conv3w_kernel, bf16 only).
+// Shapes served by the weight-stationary 3x3 kernel (conv_impl.h conv3w_kernel, 16-bit types).
 inline bool conv3w_ok(const ConvArgs& a) {
   return a.Cin == 64 && a.Cout == 64 && a.K == 576 && a.cwrap == 0 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
          !a.ln_g && (a.act == ACT_NONE || a.act == ACT_SILU) && a.Wo >= 64 && a.Wo % 64 == 0 &&
@@ -66,17 +67,20 @@ inline bool conv3w_ok(const ConvArgs& a) {
 }
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
-// init_conv (7x7, Cin 8 row-tap layout, Cout 64, bf16, plain or split-precision weights):
+// init_conv (7x7, Cin 8 row-tap layout, Cout 64, bf16 / f16, plain or split-precision weights):
 // weight-stationary persistent kernel (conv_edge.hip).
 bool conv7_ok(const ConvArgs& a);
+template <typename T>
 void conv7(const ConvArgs& a, hipStream_t st);
-// final_conv (3x3, Cin 64 -> Cout <= 4, bf16, plain or split-precision weights, Wo % 64 == 0):
+// final_conv (3x3, Cin 64 -> Cout <= 4, bf16 / f16, plain or split-precision weights, Wo % 64 == 0):
 // streaming kernel with hi/lo as separate MFMA rows (conv_edge.hip).
 bool conv3n_ok(const ConvArgs& a);
+template <typename T>
 void conv3n(const ConvArgs& a, hipStream_t st);
-// Downsample (4x4, stride 2, pad 1, bf16, Cin % 32 == 0, Cout % 64 == 0): row-band tiles with
+// Downsample (4x4, stride 2, pad 1, bf16 / f16, Cin % 32 == 0, Cout % 64 == 0): row-band tiles with
 // deinterleaved even / odd input pixels (conv_down.hip).
 bool conv_down_ok(const ConvArgs& a);
+template <typename T>
 void conv_down(const ConvArgs& a, hipStream_t st);
 int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 
@@ -102,6 +106,9 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
 // SpatialTransformer, attention.py:170-193) -> o [B*L, H*D].
 template <typename T>
 void flash_attn_d32(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st);
+// variant 1 forces the staged-tile kernel for this call (op-level test hook).
+template <typename T>
+void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale, int variant, hipStream_t st);
 extern int g_flash_old;
 
 // CLIP text tower helpers: token + positional embedding gather (ids outside [0, V) -> NaN),
@@ -126,9 +133,11 @@ void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal,
 //   la_weff   : W_eff[b][c][h*32+d] = sum_e Wout[c][h*32+e] ctx[b][h][d][e] / sum / HW
 // The to_out 1x1 conv then runs as a GEMM of softmax_d(q)*scale (fused into its A loader,
 // amode = 1) with the per-image W_eff: Wout (ctx^T q) = (Wout ctx^T) q.
+// hw_scale > 0 replaces the 1/HW factor of W_eff (f16: W_eff / HW is subnormal, so the caller
+// stores W_eff * S / HW and scales the GEMM's accumulators by 1/S, S a power of two).
 template <typename T>
 void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
-                           float* ws, hipStream_t st);
+                           float* ws, hipStream_t st, float hw_scale = 0.f);
 // Whole LinearAttention block, Residual(PreNorm(LinearAttention)) (module_util.py:27-33,
 // 89-97, 157-185), for C in {64, 128}: y = x + LN_out(to_out(ctx^T softmax_d(q))) with the
 // to_out bias and gain; weff: [B][C][128] scratch (per-image to_out weights), ws:
@@ -149,8 +158,12 @@ void small_linear(const float* x, int ldx, const float* W, const float* b, float
 // (module_util.py:41-48; scale = IRSDE.sample_scale).
 void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, double scale,
                      hipStream_t st);
-// Precision analysis: y[r*ld + c] = float(bf16(y[r*ld + c])) for r < rows, c < C.
+// Precision analysis: y[r*ld + c] = float(bf16(y[r*ld + c])) for r < rows, c < C (or the
+// fp16 rounding with DAC_EMU_FP16=1).
 void round_bf16_rows(float* y, int ld, size_t rows, int C, hipStream_t st);
+// One shared (scale, shift) row for a conv epilogue: ss[0:C] = scale_m1, ss[C:2C] = shift[c]
+// (read with ss_ld = 0 by every image).
+void ss_fill(float* ss, int C, float scale_m1, const float* shift, hipStream_t st);
 // p[0] = a, p[1] = b on the device, in stream order.
 void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st);
 // y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)

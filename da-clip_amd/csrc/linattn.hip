@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(128) la_weff(const float* ctx, const float* wo
 
 template <typename T>
 void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
-                           float* ws, hipStream_t st) {
+                           float* ws, hipStream_t st, float hw_scale) {
   const int nc = la_chunks(B, HW), CH = la_chunk_px(HW, nc);
   float* part = ws;
   float* pmax = part + (size_t)B * nc * LA_PART;
@@ -217,13 +217,15 @@ void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B
   la_kmax<T><<<dim3(nc, B), 256, 0, st>>>((const T*)qkv, pmax, HW, nc, CH);
   la_ctx<T><<<dim3(nc, B), 256, 0, st>>>((const T*)qkv, pmax, part, HW, nc, CH);
   la_reduce<<<dim3((LA_PART + 31) / 32, B), 256, 0, st>>>(part, ctx, nc);
-  la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, 1.f / (float)HW);
+  la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, hw_scale > 0.f ? hw_scale : 1.f / (float)HW);
 }
 
 template void linear_attention_weff<float>(const void*, const float*, void*, int, int, int, float*,
-                                           hipStream_t);
+                                           hipStream_t, float);
 template void linear_attention_weff<bf16>(const void*, const float*, void*, int, int, int, float*,
-                                          hipStream_t);
+                                          hipStream_t, float);
+template void linear_attention_weff<f16>(const void*, const float*, void*, int, int, int, float*,
+                                         hipStream_t, float);
 
 
 // =====================================================================================
@@ -266,6 +268,7 @@ DEV float row16_sum(float v) {
 template <typename T> DEV float exp_t(float x);
 template <> DEV float exp_t<float>(float x) { return expf(x); }
 template <> DEV float exp_t<bf16>(float x) { return __expf(x); }
+template <> DEV float exp_t<f16>(float x) { return __expf(x); }
 // bf16 handles: v_rcp_f32 / v_rsq_f32 (1 ulp) instead of the IEEE division / sqrt sequences.
 template <typename T> DEV float rcp_t(float x) { return sizeof(T) == 2 ? __builtin_amdgcn_rcpf(x) : 1.f / x; }
 template <typename T> DEV float rsq_t(float x) { return sizeof(T) == 2 ? __builtin_amdgcn_rsqf(x) : 1.f / sqrtf(x); }
@@ -300,6 +303,11 @@ template <typename T> struct OpPack;
 template <> struct OpPack<bf16> {
   bf16x8 v;
   DEV void set(int i, float f) { v[i] = (bf16)f; }
+  DEV u32x4 get() const { return __builtin_bit_cast(u32x4, v); }
+};
+template <> struct OpPack<f16> {
+  f16x8 v;
+  DEV void set(int i, float f) { v[i] = (f16)f; }
   DEV u32x4 get() const { return __builtin_bit_cast(u32x4, v); }
 };
 template <> struct OpPack<float> {
@@ -599,7 +607,7 @@ template <typename T, int C>
 __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const float* __restrict__ g,
                                                 const T* __restrict__ w, const T* __restrict__ weff,
                                                 const float* __restrict__ bout, const float* __restrict__ gout,
-                                                T* __restrict__ y, int HW, float eps) {
+                                                T* __restrict__ y, int HW, float eps, float wscale) {
   constexpr int ES = sizeof(T), VE = TypeInfo<T>::VE, KSTEP = Mma<T>::KSTEP;
   constexpr int KS = C / KSTEP;                           // q-projection k-steps
   constexpr int KO = 128 / KSTEP;                         // out-GEMM k-steps
@@ -793,7 +801,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
         const int hf = ES == 2 ? ks >> 1 : ks >> 2;
         const int j = ES == 2 ? 2 * (ks & 1) + (jj >> 2) : ks & 3;
         const int r = ES == 2 ? jj & 3 : jj;
-        o[ks][jj] = acc[hf][j][r] + bout[ks * KSTEP + lg * VE + jj];
+        o[ks][jj] = fmaf(acc[hf][j][r], wscale, bout[ks * KSTEP + lg * VE + jj]);
         so += o[ks][jj];
       }
     so = red16_sum(so);
@@ -832,7 +840,12 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
   else
     la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
   la_combine<<<dim3((LA_PART + 15) / 16, B), 256, 0, st>>>(part, ctx, nc);
-  la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, 1.f / (float)HW);
+  // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
+  // stored without the 1/HW and la_apply applies it to the fp32 accumulators (wscale).
+  const float inv_hw = 1.f / (float)HW;
+  const bool hw_late = std::is_same<T, f16>::value;
+  la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, hw_late ? 1.f : inv_hw);
+  const float wscale = hw_late ? inv_hw : 1.f;
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -846,15 +859,17 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
   nb = std::max(1, std::min(nb, (HW + 63) / 64));
   if (C == 64)
     la_apply<T, 64><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
-                                                 (T*)y, HW, 1e-5f);
+                                                 (T*)y, HW, 1e-5f, wscale);
   else
     la_apply<T, 128><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
-                                                  (T*)y, HW, 1e-5f);
+                                                  (T*)y, HW, 1e-5f, wscale);
 }
 
 template void linear_attention_fused<float>(const void*, const float*, const void*, const float*, const float*,
                                             const float*, void*, void*, int, int, int, float*, hipStream_t);
 template void linear_attention_fused<bf16>(const void*, const float*, const void*, const float*, const float*,
                                            const float*, void*, void*, int, int, int, float*, hipStream_t);
+template void linear_attention_fused<f16>(const void*, const float*, const void*, const float*, const float*,
+                                          const float*, void*, void*, int, int, int, float*, hipStream_t);
 
 }  // namespace dac

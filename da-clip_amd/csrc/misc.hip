@@ -12,6 +12,7 @@
 #include "kernels.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace dac {
 
@@ -109,15 +110,27 @@ void sinus_embedding(float* out, int R, int B, int nf, double t0, double dt, dou
 
 // Precision analysis (DAC_EMU_A, engine.cpp): round fp32 rows to bf16 in place, as a bf16
 // store followed by a load would (round to nearest even).
-__global__ void round_bf16_kernel(float* y, int ld, size_t rows, int C) {
+// fp16 != 0 rounds to IEEE half instead (DAC_EMU_FP16: what fp16 storage would cost).
+__global__ void round_bf16_kernel(float* y, int ld, size_t rows, int C, int fp16) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * C) return;
   float* p = y + (i / C) * ld + i % C;
-  *p = (float)(bf16)(*p);
+  *p = fp16 ? (float)(_Float16)(*p) : (float)(bf16)(*p);
 }
 void round_bf16_rows(float* y, int ld, size_t rows, int C, hipStream_t st) {
   const size_t n = rows * C;
-  if (n) round_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(y, ld, rows, C);
+  static const int h = getenv("DAC_EMU_FP16") ? atoi(getenv("DAC_EMU_FP16")) : 0;
+  if (n) round_bf16_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(y, ld, rows, C, h);
+}
+
+__global__ void ss_fill_kernel(float* ss, int C, float scale_m1, const float* shift) {
+  for (int c = threadIdx.x; c < C; c += 256) {
+    ss[c] = scale_m1;
+    ss[C + c] = shift ? shift[c] : 0.f;
+  }
+}
+void ss_fill(float* ss, int C, float scale_m1, const float* shift, hipStream_t st) {
+  ss_fill_kernel<<<1, 256, 0, st>>>(ss, C, scale_m1, shift);
 }
 
 // Stage the loop's noise key on the device in stream order (kernel arguments, no host
@@ -310,6 +323,7 @@ void rows_to_f32(const void* x, int ld, float* y, int R, int D, hipStream_t st) 
   template void rows_to_f32<T>(const void*, int, float*, int, int, hipStream_t);
 INST(float)
 INST(bf16)
+INST(f16)
 #undef INST
 
 // --------------------------------------------------------------------------- text tower
@@ -412,6 +426,7 @@ void degradation_probs(const float* degra, const float* text, int B, int K, int 
   template void eot_gather<T>(const int64_t*, const void*, void*, int, int, int, hipStream_t);
 TINST(float)
 TINST(bf16)
+TINST(f16)
 #undef TINST
 
 }  // namespace dac

@@ -286,6 +286,7 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
                              int, float, float*, hipStream_t);
 INST(float)
 INST(bf16)
+INST(f16)
 #undef INST
 
 }  // namespace dac

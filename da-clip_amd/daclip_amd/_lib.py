@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdaclip_hip.so")
 
-DAC_F32, DAC_BF16, DAC_FP8 = 0, 1, 2
+DAC_F32, DAC_BF16, DAC_FP8, DAC_F16 = 0, 1, 2, 3
 DAC_SRC_F32, DAC_SRC_F16, DAC_SRC_BF16 = 0, 1, 2
 DAC_POSTERIOR, DAC_SDE = 0, 1
 DAC_COSINE, DAC_LINEAR, DAC_CONSTANT = 0, 1, 2
@@ -105,7 +105,7 @@ class Handle:
         self.dtype = dtype
         self.cfg = cfg
         h = ctypes.c_void_p()
-        code = {"fp32": DAC_F32, "bf16": DAC_BF16, "fp8": DAC_FP8}[dtype]
+        code = {"fp32": DAC_F32, "bf16": DAC_BF16, "fp8": DAC_FP8, "fp16": DAC_F16}[dtype]
         with torch.cuda.device(idx):
             rc = lib().dac_create(idx, code, ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

@@ -178,7 +178,8 @@ def create_model(model_name: str, pretrained: Optional[str] = None, precision: s
     if model_name not in arch.MODEL_CONFIGS:
         raise RuntimeError(f"Model config for {model_name} not found.")
     v, t = arch.MODEL_CONFIGS[model_name]
-    dt = dtype or ("bf16" if precision in ("bf16", "pure_bf16", "amp_bf16") else "fp32")
+    dt = dtype or ("bf16" if precision in ("bf16", "pure_bf16", "amp_bf16") else
+                   "fp16" if precision in ("fp16", "pure_fp16", "amp") else "fp32")
     model = DaCLIP(v, t, device=device, dtype=dt)
     if pretrained:
         if not os.path.exists(pretrained):

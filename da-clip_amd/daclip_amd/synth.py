@@ -71,6 +71,14 @@ TRACK_KNOTS = np.arange(0, 256, 2)[:TRACK_T]      # time-embedding dims carrying
 TRACK_GAMMA = 10.0                                # hinge slope per unit t
 
 
+def tracking_projection() -> np.ndarray:
+    """A [3, 64, 3, 3]: the random 3x3 projection of the deep-path channels that forms D, each
+    kernel zero-sum over its taps, so per-channel constants of the deep features (bias-driven)
+    cancel and D is image-dependent texture with no colour cast."""
+    A = synth_tensor("tracking.D", (3, 64, 3, 3), seed=0)
+    return (A - A.mean(axis=(2, 3), keepdims=True)).astype(np.float32)
+
+
 def tracking_state_dict(sd: Mapping[str, np.ndarray], w_g1: np.ndarray, w_g2: np.ndarray,
                         k: float) -> Dict[str, np.ndarray]:
     """Synthetic nf=64 UNet weights (ch_mult [1,2,4,8], context 512) under which the reference's
@@ -83,7 +91,7 @@ def tracking_state_dict(sd: Mapping[str, np.ndarray], w_g1: np.ndarray, w_g2: np
         eps = g1(t) (x - mu) - g2(t) D,    g1 = 1/sigma_bar_t,  g2 = exp(-theta_cumsum_t dt)/sigma_bar_t
 
     so that x0 = mu + D, where D = k * (3x3 projection A of the 64 deep-path channels entering
-    final_res_block): every down / mid / up kernel shapes the output. Inside the architecture
+    final_res_block, tracking_projection()): every down / mid / up kernel shapes the output. Inside the architecture
     (DenoisingUNet_arch.py:118-174):
       * init_conv channels 0..2 copy xt - cond (7x7 centre tap 1);
       * time_mlp dims TRACK_KNOTS carry hinges GELU(GAMMA (i + 3/2 - t)), i = 0..T-1, from the
@@ -122,7 +130,7 @@ def tracking_state_dict(sd: Mapping[str, np.ndarray], w_g1: np.ndarray, w_g2: np
     fc = sd["final_conv.weight"]
     fc[:] = 0.0
     sd["final_conv.bias"][:] = 0.0
-    A = synth_tensor("tracking.D", (3, 64, 3, 3), seed=0)
+    A = tracking_projection()
     for j in range(3):
         ic[j, j, 3, 3] = 1.0
         c1[2 * j, 64 + j, 1, 1], c1[2 * j + 1, 64 + j, 1, 1] = 1.0, -1.0

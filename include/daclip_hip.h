@@ -47,8 +47,10 @@ typedef struct dac_handle dac_handle;
 
 /* compute/storage dtype. DAC_FP8: bf16 activations, and every conv / linear whose input
  * channels are a multiple of 64 runs on the block-scaled fp8 MFMA (OCP e4m3 weights and
- * on-the-fly quantized activations, one E8M0 scale per 64-element block; BASELINE configs[4]). */
-enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1, DAC_FP8 = 2 };
+ * on-the-fly quantized activations, one E8M0 scale per 64-element block; BASELINE configs[4]).
+ * DAC_F16: IEEE half weights and activations on the f16 MFMA, fp32 accumulate — the same
+ * bytes and MFMA rate as DAC_BF16 with an 11-bit instead of 8-bit significand. */
+enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1, DAC_FP8 = 2, DAC_F16 = 3 };
 enum dac_src_dtype { DAC_SRC_F32 = 0, DAC_SRC_F16 = 1, DAC_SRC_BF16 = 2 };
 enum dac_mode { DAC_POSTERIOR = 0, DAC_SDE = 1 };       /* DenoisingModel.test(mode=) */
 enum dac_schedule { DAC_COSINE = 0, DAC_LINEAR = 1, DAC_CONSTANT = 2 };
@@ -171,7 +173,8 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
 /* Op-level test hook: the SpatialTransformer self-attention core on its own (the kernel
  * dac_unet_forward runs for attention.py:170-193). qkv is [B*L, 3*H*32] (q | k | v, heads
  * of 32), out [B*L, H*32], both in `dtype` (DAC_F32 / DAC_BF16) on the current device;
- * scale = 32^-0.5. variant: 0 = the dispatcher's choice, 1 = the staged-tile kernel. */
+ * scale = 32^-0.5. variant: 0 = the dispatcher's choice, 1 = the staged-tile kernel.
+ * dtype: DAC_F32, DAC_BF16 or DAC_F16. */
 int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype, int variant,
                      void* stream);
 

@@ -213,7 +213,7 @@ def fit_tracking(base, sde, features, deep_calib):
     g1, g2 = 1.0 / sbar, 1.0 / (sbar * ea)
     w1 = np.linalg.solve(F, g1 - 1.0).astype(np.float32)
     w2 = np.linalg.solve(F, g2 - 1.0).astype(np.float32)
-    A = synth.synth_tensor("tracking.D", (3, 64, 3, 3), seed=0).astype(np.float64)
+    A = synth.tracking_projection().astype(np.float64)
     xin = deep_calib(sd0)[:, :64].astype(np.float64)
     D = torch.nn.functional.conv2d(T(xin), T(A), padding=1).numpy()
     k = float(np.float32(0.04 / D.std()))
@@ -283,8 +283,10 @@ def gen_restore():
     lq_u8 = ref_utils.tensor2img(lq.squeeze())
     inr = float(((out > 0) & (out < 1)).mean())
     psnr = ref_utils.calculate_psnr(out_u8, lq_u8)
-    print(f"restore: in-range {inr:.4f} range [{out.min():.3f},{out.max():.3f}] psnr vs lq {psnr:.3f}",
-          flush=True)
+    Dl = 255 * (out[0].astype(np.float64) - lq[0].numpy())
+    print(f"restore: in-range {inr:.4f} range [{out.min():.3f},{out.max():.3f}] psnr vs lq {psnr:.3f} "
+          f"D/level mean {Dl.mean(axis=(1, 2))} std {Dl.std(axis=(1, 2))} "
+          f"frac hist {np.histogram(Dl - np.round(Dl), bins=10)[0]}", flush=True)
     # full-length reverse_sde at 64x64 (a crop of the same image), same weights and contexts
     lq64 = lq[:, :, 96:160, 96:160].contiguous()
     s0, ssteps = restore_noise(tuple(lq64.shape), tag="sde64")
