@@ -85,8 +85,13 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
 
 // The fused res_conv rides on the bf16 v4 swapped-operand kernels: 256x64 tiles (variant 12)
 // or, for 32-pixel rows (the 32x32 level, any Cout), 128x64 tiles.
+// It mirrors every condition of the two fused conv3i_try calls in conv_dispatch (kernel choice,
+// no forced configuration, the swapped tiles' 16-byte scale / shift / bias DMA); the dispatcher
+// aborts if neither launches, so y2 is never left unwritten.
 bool conv_res_fusable(const ConvArgs& a) {
   if (!(a.w2 && a.y2 && a.ldy2 % 8 == 0 && a.bias2 == nullptr && a.Cout % 64 == 0)) return false;
+  if (g_conv3_force >= 0 || a.cwrap) return false;
+  if ((a.ss && (a.ss_ld % 4 || a.Cout % 4 || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   const int v = conv_variant(a, 3, 2);
   if (v == 12) return true;
   if (v != 20 && v != 7 && v != 11) return false;     // 128x64 v4 / v3 candidates only

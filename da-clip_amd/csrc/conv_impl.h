@@ -1409,7 +1409,8 @@ void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
 
 template <typename T, int KH, int KW, int S, int P>
 void conv_dispatch(const ConvArgs& a, hipStream_t st) {
-  // A fused second output is only requested after conv_res_fusable(a) said the v4 path takes it.
+  // A fused second output is only requested after conv_res_fusable(a) said the v4 path takes it;
+  // no path below may return without writing it.
   if (a.y2 && !(KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2 && conv_res_fusable(a))) abort();
   const int M = a.B * a.Ho * a.Wo;
   const bool batched = a.w_bstride > 0;
@@ -1458,6 +1459,9 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       conv2_kernel<T, 256, 64, 4, 2, 3, KH, KW, S, P, EPI_ALL><<<g, 512, 0, st>>>(a);
       return;
     }
+    // cwrap = 1 here means the row-tap dual layout (kernel rows wrap); the generic loaders read
+    // a nonzero cwrap as a channel wrap instead, so no other kernel may take it.
+    if (a.cwrap) abort();
   }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     const int RW = conv3_rw(a);
@@ -1477,6 +1481,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
           if (a.y2) {
             if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
+            abort();                                  // conv_res_fusable promised a fused kernel
           } else if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) {
             return;
           }

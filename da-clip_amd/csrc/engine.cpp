@@ -932,6 +932,8 @@ struct UNetNet {
     T* xin = r.alloc<T>(M0 * 8);
     if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
     T* x0 = r.alloc<T>(M0 * nf);
+    // Roles are assigned per section below; this scope restores the caller's role when the
+    // forward returns (ViT / encoder calls on the thread are unaffected).
     RoleScope rs_init(R_INIT);
     conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
     std::vector<std::pair<const void*, int>> hs;

@@ -60,7 +60,7 @@ bool conv_res_fusable(const ConvArgs& a);
 
 // Shapes served by the weight-stationary 3x3 kernel (conv_impl.h conv3w_kernel, 16-bit types).
 inline bool conv3w_ok(const ConvArgs& a) {
-  return a.Cin == 64 && a.Cout == 64 && a.K == 576 && a.cwrap == 0 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
+  return a.Cin == 64 && a.Cout == 64 && a.K == 576 && a.cwrap == 0 && !a.y2 && (!a.ss || (a.ss_ld % 4 == 0 && ((uintptr_t)a.ss & 15) == 0)) && a.zero && a.amode == 0 && a.w_bstride == 0 &&
          !a.ln_g && (a.act == ACT_NONE || a.act == ACT_SILU) && a.Wo >= 64 && a.Wo % 64 == 0 &&
          (a.C1 >= a.Cin || a.C1 % 32 == 0) && a.ldy % 8 == 0 && a.ld1 % 8 == 0 &&
          (a.C1 >= a.Cin || a.ld2 % 8 == 0) && (!a.res1 || a.ldr1 % 8 == 0) && !a.res2 && !a.bbias && !(a.ss && a.res1);   // (epi_regs16 PRE)
