@@ -339,6 +339,13 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 // the slot read in the previous iteration with tile kt+STAGES-1, then MFMA on tile kt.
 // Requires Cin % (128/sizeof(T)) == 0 so a K tile covers one (kh, kw) tap.
 typedef __attribute__((address_space(3))) void lds_void_t;
+// One 16-byte-per-lane LDS-DMA through a raw buffer descriptor (base, nbytes): voff is the
+// lane's byte offset, soff a wave-uniform one; an offset past nbytes lands zeros in LDS.
+DEV void buf_lds16(const void* base, int nbytes, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, nbytes, 0x00020000), (lds_void_t*)lds, 16,
+      voff, soff, 0, 0);
+}
 typedef __attribute__((address_space(1))) const void gbl_void_t;
 
 template <typename T, int BM, int BN, int WGM, int WGN, int STAGES, int KH, int KW, int S, int P,
@@ -846,6 +853,13 @@ conv3i_kernel(ConvArgs a, int RW) {
   const char* zero = reinterpret_cast<const char*>(a.zero);
   const int pixb = b * a.Hs * a.Ws;
 
+  // FL bit 10: buffer-resource DMA (buffer_load ... lds). Every per-lane source offset is a
+  // 32-bit table entry computed once; the chunk and kh advance ride in the scalar soffset,
+  // and padding pixels / rows past Cout carry an out-of-range offset, which the range check
+  // turns into zeros in LDS -- the main loop issues its DMA with no VALU address arithmetic.
+  // Requires ld2 == ld1 when the input is split (conv3i_buf_ok on the host).
+  constexpr bool BUF = (FL & 1024) != 0;
+  constexpr unsigned OOB = 0x80000000u;
   // A DMA: instruction j of this wave fills physical rows (wave + j*NW)*RPI + lane/SLOTS.
   int a_pix[AGX][3], a_ls[AGX];
 #pragma unroll
@@ -860,7 +874,7 @@ conv3i_kernel(ConvArgs a, int RW) {
       int pix = -1;
       if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
         pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
-      a_pix[j][kh] = pix;
+      a_pix[j][kh] = BUF ? (pix >= 0 ? (pix * a.ld1 + a_ls[j]) * ES : (int)OOB) : pix;
     }
   }
   // B DMA: instruction j of this wave fills weight rows (wave + j*NW)*RPI + lane/SLOTS
@@ -874,6 +888,7 @@ conv3i_kernel(ConvArgs a, int RW) {
     const int n = n0 + (SWAP ? (row % BN & ~63) + wperm64(row % BN & 63) : row % BN);
     b_ptr[j] = n < a.Cout ? reinterpret_cast<const T*>(a.w) + (size_t)n * a.K + (row / BN) * a.Cin
                           : nullptr;
+    if constexpr (BUF) b_ls[j] = n < a.Cout ? (int)(((size_t)n * a.K + (row / BN) * a.Cin + b_ls[j]) * ES) : (int)OOB;
   }
   // Res-weight DMA: instruction j of this wave fills rows 3*BN + (wave + j*NW)*RPI + lane/SLOTS
   // (part = local row / BN: 0 hi, 1 lo).
@@ -892,8 +907,15 @@ conv3i_kernel(ConvArgs a, int RW) {
       r_ptr[j] = (lrow < RROWS && part < nparts && n < a.Cout)
                      ? reinterpret_cast<const T*>(a.w2) + (size_t)n * a.Cin * nparts + part * a.Cin
                      : nullptr;
+      if constexpr (BUF)
+        r_ls[j] = r_ptr[j] ? (int)(((size_t)n * a.Cin * nparts + part * a.Cin + r_ls[j]) * ES) : (int)OOB;
     }
   }
+  // Buffer sizes (bytes) for the range check; the descriptors are built at each DMA from
+  // kernel-argument bases (wave-uniform by construction; the compiler hoists them).
+  const int x_bytes = BUF ? a.B * a.Hs * a.Ws * a.ld1 * ES : 0;
+  const int w_bytes = BUF ? a.Cout * a.K * ES : 0;
+  const int w2_bytes = BUF && RES && a.w2 ? a.Cout * a.Cin * nparts * ES : 0;
   // Fragment offsets (stage-relative bytes).
   const int lr = lane & 15, lg = lane >> 4;
   int aoff[NF][KSTEPS], boff[3][TN][KSTEPS];
@@ -923,6 +945,25 @@ conv3i_kernel(ConvArgs a, int RW) {
     char* st = smem + buf * STAGE;
     const int ci0 = c * BKE;
     const bool from1 = ci0 < a.C1;
+    if constexpr (BUF) {
+      const int soa = (from1 ? ci0 : ci0 - a.C1) * ES;
+#pragma unroll
+      for (int j = 0; j < AGX; ++j)
+        if (wave + j * NW < NA)                                  // wave-uniform
+          buf_lds16(from1 ? a.x1 : a.x2, x_bytes, st + (wave + j * NW) * RPI * CK, a_pix[j][kh], soa);
+      const int sob = (kh * 3 * a.Cin + ci0) * ES;
+#pragma unroll
+      for (int j = 0; j < BGX; ++j)
+        if (BGX == BGN || wave + j * NW < NB)                    // wave-uniform
+          buf_lds16(a.w, w_bytes, st + AROWS * CK + (wave + j * NW) * RPI * CK, b_ls[j], sob);
+      if constexpr (RES && kh == 1) {
+#pragma unroll
+        for (int j = 0; j < RGX; ++j)
+          if ((wave + j * NW) * RPI < RROWS)                       // wave-uniform
+            buf_lds16(a.w2, w2_bytes, st + (AROWS + 3 * BN) * CK + (wave + j * NW) * RPI * CK, r_ls[j], ci0 * ES);
+      }
+      return;
+    }
     const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) +
                      (size_t)(from1 ? ci0 : ci0 - a.C1) * ES;
     const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * ES;
@@ -1130,12 +1171,18 @@ conv3i_kernel(ConvArgs a, int RW) {
 extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
+extern int g_conv3_buf;       // v4 buffer-resource DMA (FL bit 10); DAC_CONV3_BUF=0 disables
 
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   constexpr int WTM = BM / WGM, BKE = CK / sizeof(T);
   const int RW = conv3_rw(a, BM);
   if (RW <= 0 || RW % WTM || a.Cin % BKE || (a.C1 < a.Cin && a.C1 % BKE)) return false;
+  if constexpr ((FL & 1024) != 0) {   // buffer-resource DMA: one row pitch, 31-bit byte offsets
+    constexpr size_t LIM = (size_t)1 << 30;
+    if (a.x2 && a.C1 < a.Cin && a.ld2 != a.ld1) return false;
+    if ((size_t)a.B * a.Hs * a.Ws * a.ld1 * sizeof(T) >= LIM || (size_t)a.Cout * a.K * sizeof(T) >= LIM) return false;
+  }
   if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
     if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
@@ -1166,6 +1213,12 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
       return false;
     case 41:
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st);
+      return false;
+    case 48:   // 40 / 41 with buffer-resource DMA
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024>(a, st);
+      return false;
+    case 49:
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 1024>(a, st);
       return false;
     case 42:   // diagnostics (convbench only; results are garbage): 40 without DMA / without MFMA
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32>(a, st);
@@ -1478,10 +1531,16 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         // bf16 with whole 64-channel tiles: swapped operands + register epilogue (FL bit 3),
         // 4-9 % faster than the LDS-staged epilogue at every v4 shape of the UNet.
         if constexpr (sizeof(T) == 2) {
+          // Buffer-resource DMA (FL bit 10) first; the flat-address form takes what it rejects.
+          const int nb = g_conv3_buf ? 1024 : 0;
           if (a.y2) {
+            if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
+            if (a.Cout % 64 == 0 && nb && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
             abort();                                  // conv_res_fusable promised a fused kernel
+          } else if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024>(a, st)) {
+            return;
           } else if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) {
             return;
           }
@@ -1493,7 +1552,10 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         // (The 512-wide convs stay on v3: v4 128x64 swapped tiles measured 11 % faster in
         // convbench but 3 % slower in the network.)
         if constexpr (sizeof(T) == 2)
-          if (a.Cout <= 256 && a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st)) return;
+          if (a.Cout <= 256 && a.Cout % 64 == 0) {
+            if (g_conv3_buf && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 1024>(a, st)) return;
+            if (conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st)) return;
+          }
         if (a.Cout <= 256 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 4>(a, st)) return;
       }
       // 64-byte K rows, 4 waves of 64x64 (or 64x32) wave tiles: two 24-36 KB stages, so 2-3

@@ -237,9 +237,9 @@ template void linear_attention_weff<f16>(const void*, const float*, void*, int, 
 //                 LDS -> k|v projection on MFMA (weights in registers for bf16) ->
 //                 k: online per-channel max with rescaling of the running context / sums ;
 //                 exp(k - m) and v straight from the accumulators -> ctx += P V^T (MFMA).
-//   la_combine  : rescales every chunk partial to the global channel max and sums them in
-//                 fixed order -> the same [ctx | sum] layout la_weff consumes.
-//   la_weff     : per-image to_out weights W_eff = Wout ctx^T / sum / HW.
+//   la_combine_weff : rescales every chunk partial to the global channel max, sums them in
+//                 fixed order, and folds the context into per-image to_out weights
+//                 W_eff = Wout ctx^T / sum / HW, written in la_apply's LDS image order.
 //   la_apply    : x tile -> LayerNorm -> q projection (MFMA) -> softmax over each head's 32
 //                 channels * 32^-0.5 -> out = W_eff q (MFMA, W_eff staged in LDS) -> + bias ->
 //                 LayerNorm over C (to_out.1) -> + x (Residual) -> y.
@@ -531,45 +531,122 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
   }
 }
 
-// ctx[b] = sum_c part_c * exp(max_c - max_g) (rows d), sums likewise. 16 elements x 16 chunk
-// groups per block; every thread loads its (at most 8) chunks' values and maxima up front, the
-// global max is reduced through LDS, then each group sums its terms and the 16 group sums are
-// merged in fixed order (deterministic; the chunking depends only on HW).
-__global__ void __launch_bounds__(256) la_combine(const float* part, float* ctx, int nc) {
-  constexpr int NG = 16, PER = 8;                 // la_chunks() <= 128 = NG * PER
-  __shared__ float red[NG][17];
-  const int b = blockIdx.y, el = threadIdx.x & 15, grp = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + el;
-  const bool live = i < LA_PART;
-  const int d = !live ? 0 : i < 4096 ? i / 32 : i - 4096;
-  const float* p = part + (size_t)b * nc * LA_FPART;
-  float mc[PER], v[PER];
-  float m = -INFINITY;
+// la_combine_weff: one block per (4 context rows hd0..hd0+3 of one head, image).
+//  1. ctx rows: every chunk partial rescaled to the global per-row max and summed in fixed
+//     order (the maxima go through LDS; 8 chunk groups x 32 columns, merged group by group),
+//     likewise the exp sums -- deterministic, the chunking depends only on HW.
+//  2. W_eff[c][hd] = sum_e Wout[c][h*32+e] ctx[hd][e] / sum[hd] * inv_hw for every output
+//     channel c, written straight into la_apply's LDS image order (16-bit types: row
+//     p = la_perm^-1(c), column k = la_qcol^-1(hd); fp32: natural [c][hd]), so la_apply
+//     stages it with 16-byte copies.
+template <typename T> DEV int la_prow(int c) {   // inverse of la_perm within a 64-channel half
+  if constexpr (sizeof(T) == 2) {
+    const int q = c & 63;
+    return (c & ~63) + 32 * (q >> 5) + 16 * ((q >> 2) & 1) + 4 * ((q >> 3) & 3) + (q & 3);
+  } else {
+    return c;
+  }
+}
+template <typename T> DEV int la_qcol(int qc) {  // LDS column of q channel qc in la_apply's W_eff
+  if constexpr (sizeof(T) == 2) {
+    const int u = qc & 31;
+    return (qc & ~31) + (u < 16 ? 8 * (u >> 2) + (u & 3) : 8 * ((u - 16) >> 2) + 4 + (u & 3));
+  } else {
+    return qc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) la_combine_weff(const float* __restrict__ part, const float* __restrict__ wout,
+                                                       T* __restrict__ weff, int C, int nc, float inv_hw) {
+  constexpr int NG = 8, PER = 16;                // chunk groups x chunks per group (la_chunks() <= 128)
+  __shared__ float4 sf[128];                     // per chunk: maxima of the 4 rows, then exp(max - global max)
+  __shared__ float red[NG][4][33];               // group partials: 4 rows x (32 ctx + sum)
+  __shared__ float4 mg2[2];
+  const int b = blockIdx.y, hd0 = blockIdx.x * 4, h = hd0 >> 5;
+  const int tid = threadIdx.x, grp = tid >> 5, e = tid & 31;
+  const float* pb = part + (size_t)b * nc * LA_FPART;
+  // Every global load is issued up front: this thread's chunk values, the sums, its Wout row
+  // slices and the chunk maxima -- one memory latency for the whole kernel.
+  float v[PER][4], sv[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int c = grp + NG * k;
-    const bool ok = live && c < nc;
-    mc[k] = ok ? p[(size_t)c * LA_FPART + 4096 + 128 + d] : -INFINITY;
-    v[k] = ok ? p[(size_t)c * LA_FPART + i] : 0.f;
-    m = fmaxf(m, mc[k]);
+    const bool ok = c < nc;
+    const float* pc = pb + (size_t)c * LA_FPART;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[k][r] = ok ? pc[(hd0 + r) * 32 + e] : 0.f;
+    sv[k] = (ok && e < 4) ? pc[4096 + hd0 + e] : 0.f;
   }
-  red[grp][el] = m;
-  __syncthreads();
-  float mg = red[0][el];
+  float4 wv[2][8];                               // output i = tid + 256 j: channel i >> 2
 #pragma unroll
-  for (int g = 1; g < NG; ++g) mg = fmaxf(mg, red[g][el]);
-  __syncthreads();
-  float sum = 0.f;
+  for (int j = 0; j < 2; ++j) {
+    const int i = tid + 256 * j;
+    const float* w = wout + (size_t)(i < C * 4 ? i >> 2 : 0) * 128 + h * 32;
 #pragma unroll
-  for (int k = 0; k < PER; ++k)
-    if (mc[k] != -INFINITY) sum += v[k] * expf(mc[k] - mg);
-  red[grp][el] = sum;
-  __syncthreads();
-  if (grp == 0 && live) {
-    float t = red[0][el];
+    for (int e4 = 0; e4 < 8; ++e4) wv[j][e4] = *reinterpret_cast<const float4*>(w + 4 * e4);
+  }
+  float4 m = tid < nc && tid < 128 ? *reinterpret_cast<const float4*>(pb + (size_t)tid * LA_FPART + 4096 + 128 + hd0)
+                                   : float4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  const float4 mine = m;
+  if (tid < 128) {
 #pragma unroll
-    for (int g = 1; g < NG; ++g) t += red[g][el];
-    ctx[(size_t)b * LA_PART + i] = t;
+    for (int o = 32; o >= 1; o >>= 1) {
+      m.x = fmaxf(m.x, __shfl_xor(m.x, o, 64));
+      m.y = fmaxf(m.y, __shfl_xor(m.y, o, 64));
+      m.z = fmaxf(m.z, __shfl_xor(m.z, o, 64));
+      m.w = fmaxf(m.w, __shfl_xor(m.w, o, 64));
+    }
+    if ((tid & 63) == 0) mg2[tid >> 6] = m;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const float4 a0 = mg2[0], a1 = mg2[1];
+    const float g[4] = {fmaxf(a0.x, a1.x), fmaxf(a0.y, a1.y), fmaxf(a0.z, a1.z), fmaxf(a0.w, a1.w)};
+    const float mc[4] = {mine.x, mine.y, mine.z, mine.w};
+    float f[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f[r] = mc[r] == -INFINITY ? 0.f : expf(mc[r] - g[r]);   // empty chunk: 0
+    sf[tid] = float4{f[0], f[1], f[2], f[3]};
+  }
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f}, sacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int c = grp + NG * k;
+    if (c >= nc) break;
+    const float4 f4 = sf[c];
+    const float f[4] = {f4.x, f4.y, f4.z, f4.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = fmaf(v[k][r], f[r], acc[r]);
+    sacc = fmaf(sv[k], e == 0 ? f[0] : e == 1 ? f[1] : e == 2 ? f[2] : f[3], sacc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[grp][r][e] = acc[r];
+  if (e < 4) red[grp][e][32] = sacc;
+  __syncthreads();
+  if (tid < 132) {
+    const int r = tid / 33, k = tid % 33;
+    float t = red[0][r][k];
+#pragma unroll
+    for (int g2 = 1; g2 < NG; ++g2) t += red[g2][r][k];
+    red[0][r][k] = t;
+  }
+  __syncthreads();
+  // 2. W_eff rows: thread -> (output channel c, row r).
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = tid + 256 * j;
+    if (i >= C * 4) break;
+    const int c = i >> 2, r = i & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int e4 = 0; e4 < 8; ++e4) {
+      const float* cr = &red[0][r][4 * e4];
+      s += wv[j][e4].x * cr[0] + wv[j][e4].y * cr[1] + wv[j][e4].z * cr[2] + wv[j][e4].w * cr[3];
+    }
+    s = s / red[0][r][32] * inv_hw;
+    weff[((size_t)b * C + la_prow<T>(c)) * 128 + la_qcol<T>(hd0 + r)] = from_f<T>(s);
   }
 }
 
@@ -644,24 +721,17 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
   {
     // Wq = rows 0..127 of to_qkv. W_eff[b]: LDS row p of 64-half hf = channel hf*64 + perm(p);
     // column k = 32s + 8*lg' + j holds q channel rho = 32s + (j < 4 ? 4lg' + j : 16 + 4lg' + j - 4)
-    // for bf16 (the order the repacked accumulators supply); natural order for fp32.
+    // for 16-bit types (the order the repacked accumulators supply); natural order for fp32.
+    // la_combine_weff writes W_eff in exactly this row / column order.
     constexpr int CPRQ = C / VE, CPRE = 128 / VE;
     for (int i = tid; i < 128 * CPRQ; i += 256) {
       const int r = i / CPRQ, cc = (i % CPRQ) * VE;
       *reinterpret_cast<u32x4*>(sq + qoff(r, cc / VE)) = *reinterpret_cast<const u32x4*>(w + (size_t)r * C + cc);
     }
-    const T* wb = weff + (size_t)b * C * 128;
+    const T* wb = weff + (size_t)b * C * 128;             // already in LDS image order
     for (int i = tid; i < C * CPRE; i += 256) {
       const int p = i / CPRE, k0 = (i % CPRE) * VE;
-      const int ch = (p & ~63) + la_perm<T>(p & 63);
-      T* dst = reinterpret_cast<T*>(sw + eoff(p, k0 / VE));
-      if constexpr (ES == 2) {
-        const int s = k0 >> 5, l4 = ((k0 >> 3) & 3) * 4;
-#pragma unroll
-        for (int j = 0; j < VE; ++j) dst[j] = wb[(size_t)ch * 128 + 32 * s + (j < 4 ? l4 + j : 16 + l4 + j - 4)];
-      } else {
-        *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(wb + (size_t)ch * 128 + k0);
-      }
+      *reinterpret_cast<u32x4*>(sw + eoff(p, k0 / VE)) = *reinterpret_cast<const u32x4*>(wb + (size_t)p * 128 + k0);
     }
   }
   // This lane's LayerNorm gains (channels ks*KSTEP + lg*VE + j) and epilogue terms.
@@ -834,17 +904,15 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
                             int C, float* ws, hipStream_t st) {
   const int nc = la_chunks(B, HW), CH = la_chunk_px(HW, nc);
   float* part = ws;
-  float* ctx = part + (size_t)B * nc * LA_FPART;
   if (C == 64)
     la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
   else
     la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
-  la_combine<<<dim3((LA_PART + 15) / 16, B), 256, 0, st>>>(part, ctx, nc);
   // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
   // stored without the 1/HW and la_apply applies it to the fp32 accumulators (wscale).
   const float inv_hw = 1.f / (float)HW;
   const bool hw_late = std::is_same<T, f16>::value;
-  la_weff<T><<<dim3(C, B), 128, 0, st>>>(ctx, wout, (T*)weff, C, hw_late ? 1.f : inv_hw);
+  la_combine_weff<T><<<dim3(32, B), 256, 0, st>>>(part, wout, (T*)weff, C, nc, hw_late ? 1.f : inv_hw);
   const float wscale = hw_late ? inv_hw : 1.f;
   static int ncu = 0;
   if (!ncu) {
