@@ -274,14 +274,18 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
     }
   }
 
-  f32x4 oacc[QG][2];
-  float mrun[QG], lpart[QG];
+  // Row sums of P come out of the PV MFMAs: a third O^T tile whose A operand is all ones
+  // (every row = sum over keys of P[q][key], in the same rounded P the numerator uses), so
+  // no per-score add and no cross-lane reduction at the end.
+  f32x4 oacc[QG][2], lacc[QG];
+  float mrun[QG];
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    oacc[g][0] = oacc[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    oacc[g][0] = oacc[g][1] = lacc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
     mrun[g] = -INFINITY;
-    lpart[g] = 0.f;
   }
+  const uint32_t one2 = std::is_same<T, f16>::value ? 0x3C003C00u : 0x3F803F80u;   // 1.0 in T, twice
+  const u32x4 ones = u32x4{one2, one2, one2, one2};
   const float cs = scale * 1.4426950408889634f;
   typedef short v4i16 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -333,23 +337,17 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
       tmax = red16_max(tmax);
       tmax = red32_max(tmax);
       const float mnew = fmaxf(mrun[g], tmax * cs);
-      float psum = 0.f;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
-          s[mi][r] = p;
-          psum += p;
-        }
+        for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
       // Rescale only when some query's running max moved (exact: otherwise corr == 1).
       if (DAC_FKV_SKIP == 0 || __any(mnew != mrun[g])) {
         const float corr = __builtin_amdgcn_exp2f(mrun[g] - mnew);
-        lpart[g] *= corr;
+        lacc[g] *= corr;
 #pragma unroll
         for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
       }
-      lpart[g] += psum;                          // this lane's keys only; reduced at the end
       mrun[g] = mnew;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
@@ -362,15 +360,13 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
         const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
 #pragma unroll
         for (int dm = 0; dm < 2; ++dm) Mma<T>::run(oacc[g][dm], vf[st][dm], pbu);
+        Mma<T>::run(lacc[g], ones, pbu);
       }
     }
   }
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    float l = lpart[g];
-    l = red16_sum(l);
-    l = red32_sum(l);
-    const float inv = 1.f / l;
+    const float inv = 1.f / lacc[g][0];          // every row of the ones tile holds query lr's sum
     T* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
 #pragma unroll
     for (int dm = 0; dm < 2; ++dm) {
