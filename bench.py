@@ -27,16 +27,20 @@ HBM_PEAK = 8000.0                                  # GB/s
 # Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
 # PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
 KERNEL_SYMBOL = {
-    # class 312 = v4 256x64 swapped-operand tiles, plain and with the fused res_conv output
-    (312, "bf16"): ("_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi12ELi0ELi2EEEvNS_8ConvArgsEi",
-                    "_ZN3dac13conv3i_kernelIDF16bLi256ELi64ELi4ELi1ELi64ELi2ELi28ELi0ELi2EEEvNS_8ConvArgsEi"),
-    (321, "bf16"): "void dac::conv3w_kernel<8, 4, 2>(dac::ConvArgs, int, int)",
+    # class 312 = v4 256x64 swapped-operand tiles, plain (FL 12) and with the fused res_conv
+    # output (FL 28); FL bit 10 (1036 / 1052) = the buffer-resource DMA form the dispatcher takes
+    # whenever the input has one row pitch.
     (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0ELi2EEEvNS_8ConvArgsEi",
-    (306, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
-    (307, "bf16"): "_ZN3dac12conv3_kernelIDF16bLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (306, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
     (307, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
 }
+for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
+    KERNEL_SYMBOL[(312, _dt)] = tuple(
+        f"_ZN3dac13conv3i_kernelI{_m}Li256ELi64ELi4ELi1ELi64ELi2ELi{fl}ELi0ELi2EEEvNS_8ConvArgsEi"
+        for fl in (12, 28, 1036, 1052))
+    KERNEL_SYMBOL[(321, _dt)] = f"_ZN3dac13conv3w_kernelI{_m}Li8ELi4ELi2EEEvNS_8ConvArgsEii"
+    KERNEL_SYMBOL[(306, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
+    KERNEL_SYMBOL[(307, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 

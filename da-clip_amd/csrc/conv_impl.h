@@ -874,6 +874,7 @@ conv3i_kernel(ConvArgs a, int RW) {
       int pix = -1;
       if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
         pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
+      if constexpr ((FL & 2048) != 0) pix = pix >= 0 ? (pix & 255) : pix;   // diagnostic: L2-resident A rows
       a_pix[j][kh] = BUF ? (pix >= 0 ? (pix * a.ld1 + a_ls[j]) * ES : (int)OOB) : pix;
     }
   }
@@ -1219,6 +1220,12 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
       return false;
     case 49:
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 1024>(a, st);
+      return false;
+    case 50:   // diagnostic: 48 with every A row read from a 256-pixel (L2-resident) window
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 2048>(a, st);
+      return false;
+    case 51:   // diagnostic: 50 without the epilogue
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 2048 | 128>(a, st);
       return false;
     case 42:   // diagnostics (convbench only; results are garbage): 40 without DMA / without MFMA
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 32>(a, st);
