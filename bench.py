@@ -30,9 +30,13 @@ KERNEL_SYMBOL = {
     # class 312 = v4 256x64 swapped-operand tiles, plain (FL 12) and with the fused res_conv
     # output (FL 28); FL bit 10 (1036 / 1052) = the buffer-resource DMA form the dispatcher takes
     # whenever the input has one row pitch.
-    (312, "fp32"): "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0ELi2EEEvNS_8ConvArgsEi",
-    (306, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
-    (307, "fp32"): "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi",
+    # (rocprofv3 prints fp32 instantiations demangled, the _Float16 / bfloat16 ones mangled)
+    (312, "fp32"): ("void dac::conv3i_kernel<float, 256, 64, 4, 1, 64, 2, 4, 0, 2>(dac::ConvArgs, int)",
+                    "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0ELi2EEEvNS_8ConvArgsEi"),
+    (306, "fp32"): ("void dac::conv3_kernel<float, 128, 64, 2, 2, 64>(dac::ConvArgs, int)",
+                    "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"),
+    (307, "fp32"): ("void dac::conv3_kernel<float, 128, 128, 2, 2, 64>(dac::ConvArgs, int)",
+                    "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"),
 }
 for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
     KERNEL_SYMBOL[(312, _dt)] = tuple(
