@@ -10,6 +10,7 @@ int g_conv2_force = 0;
 // Tuning aid: DAC_CONV2_FORCE32=k forces 1x1 configuration k on the small-image GEMMs only
 // (Ho*Wo <= 1024: the SpatialTransformer level), for in-network sweeps.
 int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
+int g_conv3_stagger = getenv("DAC_V4_STAGGER") ? atoi(getenv("DAC_V4_STAGGER")) : 0;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
 extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }
@@ -89,6 +90,29 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
 // It mirrors every condition of the two fused conv3i_try calls in conv_dispatch (kernel choice,
 // no forced configuration, the swapped tiles' 16-byte scale / shift / bias DMA); the dispatcher
 // aborts if neither launches, so y2 is never left unwritten.
+// Mirrors the EPI_LNF branch of conv_dispatch (conv_impl.h): 1x1, 16-bit, whole 16-byte rows,
+// tiles inside one image; GEGLU on 256x256 tiles, the rest on 64x128 swapped tiles.
+bool conv_lnf_ok(const ConvArgs& a, int elem_bytes) {
+  if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.y2 || a.up) return false;
+  if (a.Cin % 64 || a.Cout % 8 || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8)) return false;
+  if (a.x2 && a.C1 < a.Cin) return false;
+  const int HWo = a.Ho * a.Wo;
+  const bool batched = a.w_bstride > 0;
+  if (a.act == ACT_GEGLU)
+    return !a.res1 && !a.res2 && !a.bbias && !a.ss && (batched || HWo % 256 == 0) && a.Cout % 256 == 0;
+  return (a.act == ACT_NONE || a.act == ACT_SILU) && (batched || HWo % 64 == 0) && a.Cout % 128 == 0;
+}
+
+// Mirrors the EPI_GNA branch of conv_dispatch: 1x1, 16-bit, 64x128 swapped tiles inside one
+// image, groups of whole 16-byte vectors (the groupnorm_stats layout), Cin <= 1024.
+bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
+  if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.lnf_cs || a.y2 || a.up) return false;
+  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 1024 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64) return false;
+  if (a.Cin % a.gna_groups || (a.Cin / a.gna_groups) % 8 || 256 % (a.Cin / 8)) return false;
+  if (a.Cout % 128 || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8)) return false;
+  return (a.act == ACT_NONE || a.act == ACT_SILU) && (a.Ho * a.Wo) % 64 == 0;
+}
+
 bool conv_res_fusable(const ConvArgs& a) {
   if (!(a.w2 && a.y2 && a.ldy2 % 8 == 0 && a.bias2 == nullptr && a.Cout % 64 == 0)) return false;
   if (g_conv3_force >= 0 || a.cwrap) return false;

@@ -50,7 +50,9 @@ constexpr int epi_rows(int budget) {
 // stays small: the epilogue runs once per block, and every path compiled into it costs
 // instruction-cache fetches on that one pass.
 enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15,
-             EPI_LN = 16, EPI_SWAP = 32 };   // EPI_SWAP: swapped operands + epi_regs16 (conv_impl.h)
+             EPI_LN = 16, EPI_SWAP = 32,   // EPI_SWAP: swapped operands + epi_regs16 (conv_impl.h)
+             EPI_LNF = 64,                 // input LayerNorm folded into a 1x1 GEMM (ConvArgs::lnf_cs)
+             EPI_GNA = 128 };              // input GroupNorm applied in the A path (ConvArgs::gna_stats)
 
 // Per-channel epilogue terms of this lane's accumulator columns (bias, 1 + scale, shift) for a
 // tile inside image bimg; kernels that know bimg up front load them before the main loop.

@@ -360,13 +360,22 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   constexpr int KSTEPS = BKE / Mma<T>::KSTEP;
   constexpr int STAGE = (BM + BN) * 128;
   static_assert(AG >= 1 && BG >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
-  constexpr bool SWAP = (EPK & EPI_SWAP) != 0;
-  constexpr bool SLN = (EPK & EPI_LN) != 0 && SWAP;
-  static_assert(!SWAP || ((EPK == EPI_SWAP || (EPK == (EPI_SWAP | EPI_LN) && WGN == 1 && BN == 64)) && TN == 4 &&
+  // EPI_LNF (1x1 only): the input row LayerNorm folded in (ConvArgs::lnf_cs); EPE = the rest.
+  constexpr bool LNF = (EPK & EPI_LNF) != 0;
+  // EPI_GNA (1x1, swapped tiles): input GroupNorm applied to the A fragments from a per-channel
+  // (scale, shift) table of this block's image, built in LDS behind the pipeline.
+  constexpr bool GNA = (EPK & EPI_GNA) != 0;
+  constexpr int EPE = EPK & ~(EPI_LNF | EPI_GNA);
+  static_assert(!LNF || (KH == 1 && KW == 1 && sizeof(T) == 2), "LN fold: 16-bit 1x1 GEMMs");
+  static_assert(!GNA || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPE & EPI_SWAP) && !LNF), "GN in A: 16-bit 1x1 swapped");
+  constexpr bool SWAP = (EPE & EPI_SWAP) != 0;
+  constexpr bool SLN = (EPE & EPI_LN) != 0 && SWAP;
+  static_assert(!SWAP || ((EPE == EPI_SWAP || (EPE == (EPI_SWAP | EPI_LN) && WGN == 1 && BN == 64)) && TN == 4 &&
                           sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
-  constexpr int SMEM = PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES;
+  constexpr int GTAB = GNA ? 8192 : 0;                  // (scale, shift) x Cin <= 1024 floats pairs
+  constexpr int SMEM = (PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES) + GTAB;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -376,6 +385,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   const bool batched = a.w_bstride > 0;
   const int M = batched ? (tl.bz + 1) * HWo : a.B * HWo;
   const int m0 = (batched ? tl.bz * HWo : 0) + tl.bx * BM, n0 = tl.by * BN;
+  float* gtab = reinterpret_cast<float*>(smem + (SMEM - GTAB));
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   const char* zero = reinterpret_cast<const char*>(a.zero);
   const T* x1 = reinterpret_cast<const T*>(a.x1);
@@ -498,8 +508,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // LN fold: this lane's partial row sums (sum x, sum x^2) of A rows wm*WTM + i*16 + lr over
+  // the K slices it reads (8 of every 32); summed over the four lane groups after the loop.
+  float ls1[LNF ? TM : 1], ls2[LNF ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < (LNF ? TM : 1); ++i) ls1[i] = ls2[i] = 0.f;
+
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s);
+  if constexpr (GNA) {
+    // Channel c of this tile's image: s = rstd * gamma, t = beta - mean * s (tile in one image:
+    // conv_gna_ok). Its loads overlap the first stage's DMA; read after the first barrier.
+    const int bimg = m0 / HWo, cpg = a.Cin / a.gna_groups;
+    for (int c = tid; c < a.Cin; c += 64 * NW) {
+      const float* st = a.gna_stats + ((size_t)bimg * a.gna_groups + c / cpg) * 2;
+      const float sc = st[1] * a.gna_g[c];
+      gtab[2 * c] = sc;
+      gtab[2 * c + 1] = a.gna_b[c] - st[0] * sc;
+    }
+  }
   const int lr = lane & 15, lg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {
@@ -529,6 +556,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
         fb[j] = *reinterpret_cast<const u32x4*>(Bs + swz(wn * WTN + j * 16 + lr, ks * 4 + lg));
+      if constexpr (GNA) {
+        // This lane's 8 channels kt*BKE + ks*32 + lg*8 .. +7 (K = Cin for a 1x1 conv).
+        const f32x4* tp = reinterpret_cast<const f32x4*>(gtab + 2 * (kt * BKE + ks * 32 + lg * 8));
+        const f32x4 t0 = tp[0], t1 = tp[1], t2 = tp[2], t3 = tp[3];
+        const float sc[8] = {t0[0], t0[2], t1[0], t1[2], t2[0], t2[2], t3[0], t3[2]};
+        const float sh[8] = {t0[1], t0[3], t1[1], t1[3], t2[1], t2[3], t3[1], t3[3]};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          typename Vec8<T>::t v;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            float lo, hi;
+            unpack2<T>(fa[i][w], lo, hi);
+            v[2 * w] = (T)fmaf(lo, sc[2 * w], sh[2 * w]);
+            v[2 * w + 1] = (T)fmaf(hi, sc[2 * w + 1], sh[2 * w + 1]);
+          }
+          fa[i] = __builtin_bit_cast(u32x4, v);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -536,9 +582,59 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
           if constexpr (SWAP) Mma<T>::run(acc[i][j], fb[j], fa[i]);
           else Mma<T>::run(acc[i][j], fa[i], fb[j]);
         }
+      if constexpr (LNF) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            float lo, hi;
+            unpack2<T>(fa[i][w], lo, hi);
+            ls1[i] += lo + hi;
+            ls2[i] = fmaf(lo, lo, fmaf(hi, hi, ls2[i]));
+          }
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (LNF) {
+    // Row moments -> acc = rstd * (acc - mean * cs[n]), the LN'd-input GEMM before its bias.
+    const float inv_n = 1.f / (float)a.lnf_n;
+    float mu[TM], rs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float t1 = red32_sum(red16_sum(ls1[i])), t2 = red32_sum(red16_sum(ls2[i]));
+      mu[i] = t1 * inv_n;
+      rs[i] = 1.f / sqrtf(fmaxf(t2 * inv_n - mu[i] * mu[i], 0.f) + a.lnf_eps);
+    }
+    if constexpr (SWAP) {
+      // Lane (lr, lg): pixel row i*16 + lr, channels nb .. nb+15 (acc[i][e >> 2][e & 3]).
+      const int nb = n0 + wn * WTN + 16 * lg;
+      float cs[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) cs[e] = a.lnf_cs[nb + e];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e >> 2][e & 3] = rs[i] * fmaf(-mu[i], cs[e], acc[i][e >> 2][e & 3]);
+    } else {
+      // Lane (lr, lg): pixel rows i*16 + 4lg + r, channel n0 + wn*WTN + j*16 + lr; the moments
+      // of row 4lg + r sit in lane 4lg + r.
+      float cs[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + lr;
+        cs[j] = n < a.Cout ? a.lnf_cs[n] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float m = __shfl(mu[i], 4 * lg + r, 64), q = __shfl(rs[i], 4 * lg + r, 64);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j][r] = q * fmaf(-m, cs[j], acc[i][j][r]);
+        }
+    }
+  }
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
   if constexpr (SWAP) {
@@ -549,7 +645,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
     epi_regs16<T, TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
   } else {
-    conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPK>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+    conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPE>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
   }
 }
 
@@ -835,6 +931,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   using SA = RowSwz<SLOTS, TM>;
   using SB = RowSwz<SLOTS, 1>;
 
+  if (a.stagger) {
+    // First-round blocks [slots/2, slots) (slots = 2 per CU): the dispatcher deals an XCD's
+    // blocks over its CUs in turn, so block j and j + slots/2 share a CU.
+    // (stagger < 0: the alternative pairing, XCD-local neighbours j, j + 1.)
+    const int id = blockIdx.x + gridDim.x * blockIdx.y;
+    const int n = a.stagger > 0 ? a.stagger : -a.stagger;
+    if (a.stagger > 0 ? (id >= 256 && id < 512) : (id < 512 && ((id >> 3) & 1)))
+      for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(32);
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform in an SGPR
   const int wm = wave / WGN, wn = wave % WGN;
@@ -1173,6 +1278,7 @@ extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 extern int g_conv3_buf;       // v4 buffer-resource DMA (FL bit 10); DAC_CONV3_BUF=0 disables
+extern int g_conv3_stagger;   // v4 first-round stagger (ConvArgs::stagger), DAC_V4_STAGGER
 
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
@@ -1187,6 +1293,12 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
     if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
+  if (g_conv3_stagger && a.stagger != g_conv3_stagger) {
+    ConvArgs b = a;
+    b.stagger = g_conv3_stagger;
+    conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(b, RW);
+    return true;
+  }
   conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
   return true;
 }
@@ -1627,6 +1739,33 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
         return;
       }
       __builtin_trap();                          // the engine only asks for these shapes
+    }
+    if constexpr (KH == 1) if (a.gna_stats) {
+      // Input GroupNorm in the A path (conv_gna_ok mirrors this choice).
+      if constexpr (sizeof(T) == 2)
+        if (minimal(64) && a.Cout % 128 == 0 && !batched) {
+          dim3 g((Mg + 63) / 64, a.Cout / 128, gz);
+          conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_GNA><<<g, 256, 0, st>>>(a);
+          return;
+        }
+      __builtin_trap();
+    }
+    if constexpr (KH == 1) if (a.lnf_cs) {
+      // Input LayerNorm folded in (conv_lnf_ok mirrors these two choices).
+      if constexpr (sizeof(T) == 2) {
+        if (a.act == ACT_GEGLU && rows_ok && !a.res1 && !a.res2 && !a.bbias && !a.ss && (batched || HWo % 256 == 0) &&
+            a.Cout % 256 == 0) {
+          dim3 g((Mg + 255) / 256, a.Cout / 256, gz);
+          conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_GEGLU | EPI_LNF><<<g, 512, 0, st>>>(a);
+          return;
+        }
+        if (a.act != ACT_GEGLU && minimal(64) && a.Cout % 128 == 0) {
+          dim3 g((Mg + 63) / 64, a.Cout / 128, gz);
+          conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_LNF><<<g, 256, 0, st>>>(a);
+          return;
+        }
+      }
+      __builtin_trap();                          // conv_lnf_ok said a folding kernel takes it
     }
     const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho * a.Wo <= 1024) ? g_conv2_force32 : g_conv2_force;
     if constexpr (KH == 1) if (f2 > 0) {

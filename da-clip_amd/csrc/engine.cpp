@@ -48,6 +48,12 @@ static int key_role(const std::string& k) {
 template <typename T>
 static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
 // DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
+// DAC_NO_LN_FOLD=1 (read when a handle's weights are packed): SpatialTransformer norm1 / norm3
+// as separate LayerNorm launches (A/B aid; tests/test_lnfold.py).
+static bool no_ln_fold() {
+  const char* e = getenv("DAC_NO_LN_FOLD");
+  return e && atoi(e);
+}
 static bool no_res_fuse() {
   static const int v = getenv("DAC_NO_RES_FUSE") ? atoi(getenv("DAC_NO_RES_FUSE")) : 0;
   return v != 0;
@@ -353,8 +359,40 @@ struct Packer {
     cw.w = pool.upload(h.data(), h.size() * 2);
     return cw;
   }
+  // Input-LayerNorm fold of a packed [O][K] 1x1 weight p (ConvArgs::lnf_cs; 16-bit handles):
+  // w = p diag(g) stored in T, cs[n] = sum_k w[n][k] over the STORED (rounded) values, bias
+  // = pb + p beta. LN(x) p^T + pb = rstd (x w^T - mean cs) + bias.
+  struct Folded { ConvW cw; const float* cs = nullptr; };
+  Folded fold_ln(const ConvW& base, const std::vector<float>& p, int O, int K, const std::string& gkey,
+                 const std::string& bkey, const std::vector<float>* pb) {
+    Folded f;
+    f.cw = base;
+    f.cw.w8 = nullptr; f.cw.ws8 = nullptr; f.cw.kp8 = 0;
+    if constexpr (sizeof(T) != 2) return f;
+    const HostW* g = ws.get(gkey, {K});
+    const HostW* be = ws.get(bkey, {K});
+    if (!g || !be || p.size() != (size_t)O * K) return f;
+    std::vector<float> w(p.size()), cs(O), bias(O);
+    for (int o = 0; o < O; ++o)
+      for (int k = 0; k < K; ++k) w[(size_t)o * K + k] = p[(size_t)o * K + k] * g->v[k];
+    using C = typename CodecOf<T>::type;
+    const std::vector<uint16_t> h = quantize16<C>(w, 1, K);
+    for (int o = 0; o < O; ++o) {
+      double c = 0, b = pb ? (*pb)[o] : 0.0;
+      for (int k = 0; k < K; ++k) {
+        c += C::dec(h[(size_t)o * K + k]);
+        b += (double)p[(size_t)o * K + k] * be->v[k];
+      }
+      cs[o] = (float)c;
+      bias[o] = (float)b;
+    }
+    f.cw.w = pool.upload(h.data(), h.size() * 2);
+    f.cw.b = (const float*)pool.upload(bias.data(), bias.size() * 4);
+    f.cs = (const float*)pool.upload(cs.data(), cs.size() * 4);
+    return f;
+  }
   // Row-concatenation of several [Oi][I] linears (q | k | v) into one GEMM.
-  ConvW concat(const std::vector<std::string>& keys, int O, int I) {
+  ConvW concat(const std::vector<std::string>& keys, int O, int I, std::vector<float>* keep = nullptr) {
     ConvW cw;
     cw.cout = O * (int)keys.size(); cw.cin = cw.cin_real = I;
     std::vector<float> p;
@@ -367,12 +405,14 @@ struct Packer {
     if (ok) {
       cw.w = upload_T(p, keys[0]);
       make_fp8(cw, p, cw.cout, I);
+      if (keep) *keep = std::move(p);
     }
     return cw;
   }
   // GEGLU proj [2F][I] (+bias): rows reordered so each 32-row group holds 16 "x" rows then
   // their 16 "gate" rows; the conv epilogue pairs accumulator tiles j, j+1.
-  ConvW geglu(const std::string& key, const std::string& bkey, int F, int I) {
+  ConvW geglu(const std::string& key, const std::string& bkey, int F, int I, std::vector<float>* keep = nullptr,
+              std::vector<float>* keep_b = nullptr) {
     ConvW cw;
     cw.cout = 2 * F; cw.cin = cw.cin_real = I;
     const HostW* w = ws.get(key, {2 * F, I});
@@ -389,6 +429,8 @@ struct Packer {
     cw.w = upload_T(p, key);
     make_fp8(cw, p, 2 * F, I);
     cw.b = (const float*)pool.upload(pb.data(), pb.size() * 4);
+    if (keep) *keep = std::move(p);
+    if (keep_b) *keep_b = std::move(pb);
     return cw;
   }
 };
@@ -424,6 +466,10 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.ss = e.ss; a.ss_ld = e.ss_ld; a.res1 = e.res1; a.ldr1 = e.ldr1; a.res2 = e.res2;
   a.ldr2 = e.ldr2; a.bbias = e.bbias; a.bb_ld = e.bb_ld; a.y = y; a.ldy = ldy; a.act = e.act;
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
+  a.lnf_cs = e.lnf_cs; a.lnf_n = e.lnf_n; a.lnf_eps = e.lnf_eps;
+  a.gna_stats = e.gna_stats; a.gna_g = e.gna_g; a.gna_b = e.gna_b; a.gna_groups = e.gna_groups;
+  if (a.lnf_cs && !conv_lnf_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: LN fold requested on a shape without a folding kernel");
+  if (a.gna_stats && !conv_gna_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: GroupNorm A path requested on a shape without such a kernel");
   const double M = (double)B * a.Ho * a.Wo;
   double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   Profiler* p = r.prof;
@@ -569,7 +615,9 @@ struct UNetNet {
               // attn2 without a context is self-attention over norm2(x) (attention.py:174);
               // it needs context_dim == C, as in the reference (to_k / to_v take C inputs).
               bool self_ok = false; ConvW qkv2, o2; const float *n2w = nullptr, *n2b = nullptr;
-              int cc_off = 0; };
+              int cc_off = 0;
+              // norm1 / norm3 folded into q|k|v and the GEGLU proj (16-bit handles, not fp8).
+              ConvW qkv_f, ff1_f; const float *qkv_cs = nullptr, *ff1_cs = nullptr; };
   struct Attn { bool st = false; LA la; ST s; };
   struct Level { RB b1, b2; Attn at; ConvW samp; };
 
@@ -633,9 +681,15 @@ struct UNetNet {
     s.gnb = P.f32(f + "norm.bias", {C});
     s.pin = P.conv(f + "proj_in.weight", C, C, 1, 1, f + "proj_in.bias");
     const std::string b = f + "transformer_blocks.0.";
-    s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C);
+    std::vector<float> pq, pf, pfb;
+    s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C, &pq);
     s.o = P.linear(b + "attn1.to_out.0.weight", C, C, b + "attn1.to_out.0.bias");
-    s.ff1 = P.geglu(b + "ff.net.0.proj.weight", b + "ff.net.0.proj.bias", 4 * C, C);
+    s.ff1 = P.geglu(b + "ff.net.0.proj.weight", b + "ff.net.0.proj.bias", 4 * C, C, &pf, &pfb);
+    if (sizeof(T) == 2 && !P.fp8 && !no_ln_fold()) {
+      auto fq = P.fold_ln(s.qkv, pq, 3 * C, C, b + "norm1.weight", b + "norm1.bias", nullptr);
+      auto ff = P.fold_ln(s.ff1, pf, 8 * C, C, b + "norm3.weight", b + "norm3.bias", &pfb);
+      if (fq.cs && ff.cs) { s.qkv_f = fq.cw; s.qkv_cs = fq.cs; s.ff1_f = ff.cw; s.ff1_cs = ff.cs; }
+    }
     s.ff2 = P.linear(b + "ff.net.2.weight", C, 4 * C, b + "ff.net.2.bias");
     // attn2 attends to ONE context token: softmax over a single key is exactly 1, so its
     // output is to_out(to_v(ctx)) for every query; to_q / to_k / norm2 cannot affect it
@@ -847,6 +901,18 @@ struct UNetNet {
     return y;
   }
 
+  // The dispatcher has an LN-folding kernel for this 1x1 GEMM shape (conv_lnf_ok).
+  static bool gna_fits(int C, int Cout, int HW) {
+    ConvArgs a{};
+    a.zero = &a; a.Cin = a.C1 = a.K = C; a.Cout = a.ldy = Cout; a.gna_groups = 32; a.Ho = HW; a.Wo = 1;
+    return !no_ln_fold() && conv_gna_ok(a, (int)sizeof(T));
+  }
+  static bool lnf_fits(int Cin, int Cout, int act, int HW) {
+    ConvArgs a{};
+    a.zero = &a; a.Cin = a.C1 = Cin; a.Cout = Cout; a.act = act; a.ldy = act == ACT_GEGLU ? Cout / 2 : Cout;
+    a.Ho = HW; a.Wo = 1;
+    return conv_lnf_ok(a, (int)sizeof(T));
+  }
   const void* sptrans(Run& r, const ST& s, const void* x, int C, int B, int H, int W,
                       const float* cc) {
     RoleScope rs(g_role == R_MID ? R_MID : R_ST);
@@ -854,18 +920,34 @@ struct UNetNet {
     const size_t M = (size_t)B * L;
     T* xn = r.alloc<T>(M * C);
     ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
-    T* gn = r.alloc<T>(M * C);
     // GroupNorm workspace: partial moments [B][32 groups][GN_CHUNKS = 32][3], then the merged
     // (mean, rstd) [B][32][2].
     float* stats = r.alloc<float>((size_t)B * 32 * (32 * 3 + 2));
-    if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
-    emu_round<T>(r, gn, C, M, C);
     T* hh = r.alloc<T>(M * C);
-    conv_call<T>(r, s.pin, gn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, Epi());
-    T* a = r.alloc<T>(M * C);
-    ln<T>(r, hh, C, a, C, nullptr, 0, s.n1w, s.n1b, (int)M, C, 1e-5f);
+    if (gna_fits(C, C, L)) {
+      // proj_in reads xn and applies the GroupNorm to its A fragments (no normalised copy).
+      Epi ep;
+      ep.gna_stats = stats + (size_t)B * 32 * 32 * 3;
+      ep.gna_g = s.gnw; ep.gna_b = s.gnb; ep.gna_groups = 32;
+      if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, r.st);
+      conv_call<T>(r, s.pin, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, ep);
+    } else {
+      T* gn = r.alloc<T>(M * C);
+      if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
+      emu_round<T>(r, gn, C, M, C);
+      conv_call<T>(r, s.pin, gn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, Epi());
+    }
     T* qkv = r.alloc<T>(M * 3 * C);
-    conv_call<T>(r, s.qkv, a, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 3 * C, Epi());
+    if (s.qkv_cs && lnf_fits(C, 3 * C, ACT_NONE, L)) {
+      // norm1 folded into q|k|v: the GEMM reads hh and takes its row moments itself.
+      Epi ef;
+      ef.lnf_cs = s.qkv_cs; ef.lnf_n = C;
+      conv_call<T>(r, s.qkv_f, hh, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 3 * C, ef);
+    } else {
+      T* a = r.alloc<T>(M * C);
+      ln<T>(r, hh, C, a, C, nullptr, 0, s.n1w, s.n1b, (int)M, C, 1e-5f);
+      conv_call<T>(r, s.qkv, a, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 3 * C, Epi());
+    }
     T* o = r.alloc<T>(M * C);
     r.flops += 4.0 * B * (double)L * L * C;     // QK^T and PV
     if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, 0.17677669529663687f, r.st);
@@ -897,12 +979,17 @@ struct UNetNet {
       conv_call<T>(r, s.o2, o2, C, C, nullptr, 0, B, H, W, 0, 1, 0, h3, C, e3);
       h2 = h3;
     }
-    T* f = r.alloc<T>(M * C);
-    ln<T>(r, h2, C, f, C, nullptr, 0, s.n3w, s.n3b, (int)M, C, 1e-5f);
     T* g = r.alloc<T>(M * 4 * C);
     Epi eg;
     eg.act = ACT_GEGLU;
-    conv_call<T>(r, s.ff1, f, C, C, nullptr, 0, B, H, W, 0, 1, 0, g, 4 * C, eg);
+    if (s.ff1_cs && lnf_fits(C, 8 * C, ACT_GEGLU, L)) {
+      eg.lnf_cs = s.ff1_cs; eg.lnf_n = C;                     // norm3 folded into the GEGLU proj
+      conv_call<T>(r, s.ff1_f, h2, C, C, nullptr, 0, B, H, W, 0, 1, 0, g, 4 * C, eg);
+    } else {
+      T* f = r.alloc<T>(M * C);
+      ln<T>(r, h2, C, f, C, nullptr, 0, s.n3w, s.n3b, (int)M, C, 1e-5f);
+      conv_call<T>(r, s.ff1, f, C, C, nullptr, 0, B, H, W, 0, 1, 0, g, 4 * C, eg);
+    }
     T* h4 = r.alloc<T>(M * C);
     Epi e4;
     e4.res1 = h2; e4.ldr1 = C;

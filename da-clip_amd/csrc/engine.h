@@ -126,6 +126,15 @@ struct Epi {
   const ConvW* fuse1x1 = nullptr;
   void* y2 = nullptr;
   int ldy2 = 0;
+  // 1x1 GEMMs with the input row LayerNorm folded into the weights (ConvArgs::lnf_cs).
+  const float* lnf_cs = nullptr;
+  int lnf_n = 0;
+  float lnf_eps = 1e-5f;
+  // 1x1 GEMMs applying the input GroupNorm in their A path (ConvArgs::gna_stats).
+  const float* gna_stats = nullptr;
+  const float* gna_g = nullptr;
+  const float* gna_b = nullptr;
+  int gna_groups = 0;
 };
 
 template <typename T>

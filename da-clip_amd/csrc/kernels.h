@@ -54,7 +54,35 @@ struct ConvArgs {
   const float* bias2;
   int w2_dual;
   void* y2; int ldy2;
+  // v4 3x3 tiles (tuning experiment, DAC_V4_STAGGER): first-round blocks of the upper half of
+  // the co-resident slots start `stagger` x 2048 clocks late, so two blocks sharing a CU run
+  // their epilogues out of phase. 0 = off.
+  int stagger;
+  // Row LayerNorm of the INPUT folded into a 1x1 GEMM (SpatialTransformer norm1 -> q|k|v and
+  // norm3 -> GEGLU proj, attention.py:253-261): the weights are pre-multiplied by the LN gain
+  // (w = W diag(g)), bias = b + W beta, and the kernel takes the row moments of x from its own
+  // A fragments, then y = rstd * (x.w^T - mean * lnf_cs[n]) + bias with lnf_cs[n] = sum_k w[n][k]
+  // (of the stored, rounded weights). lnf_n = channels in the mean, lnf_eps the LN epsilon.
+  const float* lnf_cs;
+  int lnf_n;
+  float lnf_eps;
+  // GroupNorm of the INPUT applied in a 1x1 GEMM's A path (SpatialTransformer norm ->
+  // proj_in, attention.py:76-77, 239-241): the A fragments are mapped x -> x * s + t per
+  // channel, s = rstd(b, g) * gamma, t = beta - mean(b, g) * s, rounded back to T (what a
+  // separate GroupNorm pass would have stored). gna_stats = [B][groups][mean, rstd].
+  const float* gna_stats;
+  const float* gna_g;
+  const float* gna_b;
+  int gna_groups;
 };
+// The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
+bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
+// ... and a kernel applying the input GroupNorm in its A path (ConvArgs::gna_stats).
+bool conv_gna_ok(const ConvArgs& a, int elem_bytes);
+// GroupNorm statistics only (norm.hip): the (mean, rstd) table groupnorm() applies, at
+// part + B * groups * GN_CHUNKS * 3 (returned).
+template <typename T>
+const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part, hipStream_t st);
 // The dispatcher can fuse a_w2/y2 into this 3x3 conv (bf16 v4 256x64 swapped-operand tiles).
 bool conv_res_fusable(const ConvArgs& a);
 

@@ -279,7 +279,18 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
       (const T*)x, (T*)y, part + (size_t)B * groups * GN_CHUNKS * 3, g, b, HW, C, groups, nvec);
 }
 
+template <typename T>
+const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part, hipStream_t st) {
+  constexpr int VE = TypeInfo<T>::VE;
+  const int NV = C / VE;
+  if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64) abort();   // conv_gna_ok checks this
+  gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
+  gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
+  return part + (size_t)B * groups * GN_CHUNKS * 3;
+}
+
 #define INST(T)                                                                              \
+  template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, hipStream_t); \
   template void layernorm<T>(const void*, int, void*, int, const void*, int, const float*,  \
                              const float*, int, int, float, hipStream_t);                   \
   template void groupnorm<T>(const void*, void*, const float*, const float*, int, int, int, \

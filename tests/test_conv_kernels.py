@@ -28,3 +28,18 @@ def test_conv3x3_kernels_match_naive_reference():
     # The shapes that take the v5 kernel by default really ran it (variant 21).
     v5 = [l for l in rows if re.search(r"64->64 .*f-1\s+variant 21", l)]
     assert len(v5) == 4, "\n".join(rows)
+
+
+@pytest.mark.gpu
+def test_ln_folded_gemms_match_host_reference():
+    """SpatialTransformer norm1 -> q|k|v and norm3 -> GEGLU proj as ONE GEMM each (EPI_LNF: the
+    LN gain folded into the weights, the row moments taken from the kernel's own A fragments,
+    engine.cpp Packer::fold_ln) against a host fp64 LayerNorm + GEMM (+ GEGLU) with the exact
+    weights, on rows offset by several standard deviations (attention.py:253-261; LN eps 1e-5).
+    Bound 1e-2 max-rel: bf16 operands and output (measured figures in the printout)."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "lnf", "3"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l for l in out.stdout.splitlines() if "check rel" in l]
+    assert len(rows) == 6 and all(l.rstrip().endswith("OK") for l in rows), out.stdout

@@ -200,8 +200,198 @@ static int fp8_check() {
   return fails;
 }
 
+// Input-LayerNorm fold (ConvArgs::lnf_cs, EPI_LNF): LN(x) W^T + b of the SpatialTransformer's
+// norm1 -> q|k|v and norm3 -> GEGLU proj against a host fp64 reference of the UNfolded op
+// (LayerNorm eps 1e-5 with gain / bias, then the exact-weight GEMM; GEGLU x * gelu(gate) over
+// the 16-row interleaved weight layout). x has a per-row offset of several standard deviations
+// so the kernel's single-pass moments and its mean * colsum subtraction are exercised.
+static int lnf_check(int iters) {
+  struct SL { const char* name; int M, C, N, geglu; };
+  const SL shapes[] = {{"lnf qkv 512->1536", 8192, 512, 1536, 0}, {"lnf qkv 256->768", 8192, 256, 768, 0},
+                       {"lnf geglu 512->4096", 8192, 512, 4096, 1}, {"lnf geglu 256->2048", 8192, 256, 2048, 1}};
+  int fails = 0;
+  for (const SL& sh : shapes) {
+    const int M = sh.M, C = sh.C, N = sh.N, NO = sh.geglu ? N / 2 : N;
+    uint32_t h = 777 + C + N;
+    auto rnd = [&]() { h = h * 1664525u + 1013904223u; return ((h >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb((size_t)M * C);
+    std::vector<double> xf((size_t)M * C);
+    for (int m = 0; m < M; ++m) {
+      const float off = 6.f * rnd(), sc = 0.5f + std::fabs(rnd()) * 2.f;
+      for (int c = 0; c < C; ++c) {
+        xb[(size_t)m * C + c] = (bf16)(off + sc * rnd());
+        xf[(size_t)m * C + c] = bf2f(xb[(size_t)m * C + c]);
+      }
+    }
+    std::vector<float> g(C), be(C), w((size_t)N * C), b(N);
+    for (auto& v : g) v = 1.f + 0.5f * rnd();
+    for (auto& v : be) v = 0.2f * rnd();
+    for (auto& v : w) v = rnd() * 0.1f;
+    for (auto& v : b) v = 0.1f * rnd();
+    // Folded operands (what engine.cpp Packer::fold_ln stores): w' = bf16(w g), cs = sum w'.
+    std::vector<bf16> wf((size_t)N * C);
+    std::vector<float> cs(N), bf(N);
+    for (int n = 0; n < N; ++n) {
+      double c = 0, bb = b[n];
+      for (int k = 0; k < C; ++k) {
+        wf[(size_t)n * C + k] = (bf16)(w[(size_t)n * C + k] * g[k]);
+        c += bf2f(wf[(size_t)n * C + k]);
+        bb += (double)w[(size_t)n * C + k] * be[k];
+      }
+      cs[n] = (float)c;
+      bf[n] = (float)bb;
+    }
+    // Reference (fp64): LN rows, GEMM with the exact weights, bias, GEGLU pairing.
+    std::vector<double> ln((size_t)M * C), ref((size_t)M * NO);
+    for (int m = 0; m < M; ++m) {
+      double mu = 0, var = 0;
+      for (int c = 0; c < C; ++c) mu += xf[(size_t)m * C + c];
+      mu /= C;
+      for (int c = 0; c < C; ++c) { const double d = xf[(size_t)m * C + c] - mu; var += d * d; }
+      const double rs = 1.0 / std::sqrt(var / C + 1e-5);
+      for (int c = 0; c < C; ++c) ln[(size_t)m * C + c] = (xf[(size_t)m * C + c] - mu) * rs * g[c] + be[c];
+    }
+    std::vector<double> yr(N);
+    for (int m = 0; m < M; ++m) {
+      for (int n = 0; n < N; ++n) {
+        double acc = b[n];
+        const double* lp = &ln[(size_t)m * C];
+        const float* wp = &w[(size_t)n * C];
+        for (int k = 0; k < C; ++k) acc += lp[k] * wp[k];
+        yr[n] = acc;
+      }
+      for (int o = 0; o < NO; ++o) {
+        if (!sh.geglu) { ref[(size_t)m * NO + o] = yr[o]; continue; }
+        const int grp = o / 16, s = o % 16;                        // output channel o of group grp
+        const double xv = yr[32 * grp + s], gv = yr[32 * grp + 16 + s];
+        ref[(size_t)m * NO + o] = xv * 0.5 * gv * (1.0 + std::erf(gv / std::sqrt(2.0)));
+      }
+    }
+    void *dx, *dw, *dy, *dz; float *dcs, *dbf;
+    CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dw, wf.size() * 2)); CK(hipMalloc(&dy, (size_t)M * NO * 2));
+    CK(hipMalloc(&dz, 256)); CK(hipMalloc(&dcs, N * 4)); CK(hipMalloc(&dbf, N * 4));
+    CK(hipMemset(dz, 0, 256));
+    CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, wf.data(), wf.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dcs, cs.data(), N * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dbf, bf.data(), N * 4, hipMemcpyHostToDevice));
+    ConvArgs a{};
+    a.x1 = dx; a.ld1 = C; a.C1 = C; a.Cin = C; a.Hs = 32; a.Ws = M / 32 / 8; a.B = 8;
+    a.Ho = a.Hs; a.Wo = a.Ws; a.Cout = N; a.K = C; a.w = dw; a.bias = dbf; a.y = dy; a.ldy = NO;
+    a.zero = dz; a.act = sh.geglu ? 3 : 0;
+    a.lnf_cs = dcs; a.lnf_n = C; a.lnf_eps = 1e-5f;
+    if (!conv_lnf_ok(a, 2)) { printf("%-24s not eligible\n", sh.name); ++fails; continue; }
+    conv<bf16>(a, 1, 1, 1, 0, 0);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) conv<bf16>(a, 1, 1, 1, 0, 0);
+    CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<bf16> yb((size_t)M * NO);
+    CK(hipMemcpy(yb.data(), dy, yb.size() * 2, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    int nnan = 0;
+    for (size_t i = 0; i < yb.size(); ++i) {
+      const double v = bf2f(yb[i]);
+      if (!std::isfinite(v)) ++nnan;
+      md = std::max(md, std::fabs(v - ref[i]));
+      mx = std::max(mx, std::fabs(ref[i]));
+    }
+    const bool ok = nnan == 0 && md / mx < 1e-2;
+    const double us = ms * 1e3 / iters, fl = 2.0 * M * N * C;
+    printf("%-24s %8.1f us %7.1f TF/s  check rel %.2e %s\n", sh.name, us, fl / us / 1e6, md / mx, ok ? "OK" : "FAIL");
+    fails += !ok;
+    CK(hipFree(dx)); CK(hipFree(dw)); CK(hipFree(dy)); CK(hipFree(dz)); CK(hipFree(dcs)); CK(hipFree(dbf));
+  }
+  // GroupNorm(32, eps 1e-6) applied in the A path of proj_in (EPI_GNA), stats from the host.
+  struct SG { const char* name; int C; };
+  const SG gshapes[] = {{"gna proj_in 512->512", 512}, {"gna proj_in 256->256", 256}};
+  for (const SG& sh : gshapes) {
+    const int B = 8, HW = 1024, M = B * HW, C = sh.C, N = C, G = 32, cpg = C / G;
+    uint32_t h = 4242 + C;
+    auto rnd = [&]() { h = h * 1664525u + 1013904223u; return ((h >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb((size_t)M * C), wb((size_t)N * C);
+    std::vector<float> gm(C), bt(C), bias(N), st((size_t)B * G * 2);
+    for (int c = 0; c < C; ++c) { gm[c] = 1.f + 0.5f * rnd(); bt[c] = 0.3f * rnd(); }
+    for (int b = 0; b < B; ++b)
+      for (int c = 0; c < C; ++c) {
+        const float off = 4.f * std::sin(0.37f * (b * C + c)), sc = 1.f + 0.5f * std::cos(0.11f * c);
+        for (int p = 0; p < HW; ++p) xb[((size_t)b * HW + p) * C + c] = (bf16)(off + sc * rnd());
+      }
+    for (auto& v : wb) v = (bf16)(0.1f * rnd());
+    for (auto& v : bias) v = 0.1f * rnd();
+    std::vector<double> gn((size_t)M * C);
+    for (int b = 0; b < B; ++b)
+      for (int g = 0; g < G; ++g) {
+        double s1 = 0, s2 = 0;
+        for (int p = 0; p < HW; ++p)
+          for (int c = g * cpg; c < (g + 1) * cpg; ++c) s1 += bf2f(xb[((size_t)b * HW + p) * C + c]);
+        const double mu = s1 / (HW * cpg);
+        for (int p = 0; p < HW; ++p)
+          for (int c = g * cpg; c < (g + 1) * cpg; ++c) { const double d = bf2f(xb[((size_t)b * HW + p) * C + c]) - mu; s2 += d * d; }
+        const double rs = 1.0 / std::sqrt(s2 / (HW * cpg) + 1e-6);
+        st[((size_t)b * G + g) * 2] = (float)mu;
+        st[((size_t)b * G + g) * 2 + 1] = (float)rs;
+        for (int p = 0; p < HW; ++p)
+          for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            const size_t i = ((size_t)b * HW + p) * C + c;
+            gn[i] = (bf2f(xb[i]) - mu) * rs * gm[c] + bt[c];
+          }
+      }
+    std::vector<double> ref((size_t)M * N);
+    for (int m = 0; m < M; ++m)
+      for (int n = 0; n < N; ++n) {
+        double acc = bias[n];
+        for (int k = 0; k < C; ++k) acc += gn[(size_t)m * C + k] * bf2f(wb[(size_t)n * C + k]);
+        ref[(size_t)m * N + n] = acc;
+      }
+    void *dx, *dw, *dy, *dz; float *dst, *dg, *db, *dbias;
+    CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dw, wb.size() * 2)); CK(hipMalloc(&dy, (size_t)M * N * 2));
+    CK(hipMalloc(&dz, 256)); CK(hipMalloc(&dst, st.size() * 4)); CK(hipMalloc(&dg, C * 4)); CK(hipMalloc(&db, C * 4));
+    CK(hipMalloc(&dbias, N * 4));
+    CK(hipMemset(dz, 0, 256));
+    CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dst, st.data(), st.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, gm.data(), C * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, bt.data(), C * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dbias, bias.data(), N * 4, hipMemcpyHostToDevice));
+    ConvArgs a{};
+    a.x1 = dx; a.ld1 = C; a.C1 = C; a.Cin = C; a.Hs = 32; a.Ws = 32; a.B = B; a.Ho = 32; a.Wo = 32;
+    a.Cout = N; a.K = C; a.w = dw; a.bias = dbias; a.y = dy; a.ldy = N; a.zero = dz;
+    a.gna_stats = dst; a.gna_g = dg; a.gna_b = db; a.gna_groups = G;
+    if (!conv_gna_ok(a, 2)) { printf("%-24s not eligible\n", sh.name); ++fails; continue; }
+    conv<bf16>(a, 1, 1, 1, 0, 0);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) conv<bf16>(a, 1, 1, 1, 0, 0);
+    CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<bf16> yb((size_t)M * N);
+    CK(hipMemcpy(yb.data(), dy, yb.size() * 2, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    int nnan = 0;
+    for (size_t i = 0; i < yb.size(); ++i) {
+      const double v = bf2f(yb[i]);
+      if (!std::isfinite(v)) ++nnan;
+      md = std::max(md, std::fabs(v - ref[i]));
+      mx = std::max(mx, std::fabs(ref[i]));
+    }
+    const bool ok = nnan == 0 && md / mx < 1e-2;
+    const double us = ms * 1e3 / iters, fl = 2.0 * M * N * C;
+    printf("%-24s %8.1f us %7.1f TF/s  check rel %.2e %s\n", sh.name, us, fl / us / 1e6, md / mx, ok ? "OK" : "FAIL");
+    fails += !ok;
+    CK(hipFree(dx)); CK(hipFree(dw)); CK(hipFree(dy)); CK(hipFree(dz)); CK(hipFree(dst)); CK(hipFree(dg));
+    CK(hipFree(db)); CK(hipFree(dbias));
+  }
+  return fails;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
+  if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
   int iters = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 && argv[2][0] ? argv[2] : nullptr;   // substring filter
   const bool check = argc > 3 && !strcmp(argv[3], "check");
