@@ -302,7 +302,7 @@ struct Packer {
   // kwp > kw: each kernel row is padded to kwp taps (zero weights), so one K tile of
   // kwp * cin elements is one kernel row (the bf16 7x7 init conv: 8 taps x 8 channels).
   ConvW conv(const std::string& key, int O, int C, int kh, int kw, const std::string& bkey = "",
-             bool linear2d = false, int kwp = 0) {
+             bool linear2d = false, int kwp = 0, std::vector<float>* keep = nullptr) {
     ConvW cw;
     cw.cout = O; cw.cin_real = C; cw.cin = pad_to(C, VE); cw.kh = kh; cw.kw = kw;
     cw.kwp = kwp > kw ? kwp : 0;
@@ -318,6 +318,7 @@ struct Packer {
             p[(((size_t)o * kh + y) * kws + x) * cw.cin + c] = w->v[(((size_t)o * C + c) * kh + y) * kw + x];
     cw.w = upload_T(p, key, kh * kws, cw.cin);
     make_fp8(cw, p, O, kh * kws * cw.cin);
+    if (keep) *keep = std::move(p);
     return cw;
   }
   ConvW linear(const std::string& key, int O, int I, const std::string& bkey = "") {
@@ -363,15 +364,17 @@ struct Packer {
   // w = p diag(g) stored in T, cs[n] = sum_k w[n][k] over the STORED (rounded) values, bias
   // = pb + p beta. LN(x) p^T + pb = rstd (x w^T - mean cs) + bias.
   struct Folded { ConvW cw; const float* cs = nullptr; };
+  // bkey empty: a gain-only LayerNorm (module_util.py:77-86); gshape: the gain's stored shape.
   Folded fold_ln(const ConvW& base, const std::vector<float>& p, int O, int K, const std::string& gkey,
-                 const std::string& bkey, const std::vector<float>* pb) {
+                 const std::string& bkey, const std::vector<float>* pb, std::vector<int64_t> gshape = {}) {
     Folded f;
     f.cw = base;
     f.cw.w8 = nullptr; f.cw.ws8 = nullptr; f.cw.kp8 = 0;
     if constexpr (sizeof(T) != 2) return f;
-    const HostW* g = ws.get(gkey, {K});
-    const HostW* be = ws.get(bkey, {K});
-    if (!g || !be || p.size() != (size_t)O * K) return f;
+    if (gshape.empty()) gshape = {K};
+    const HostW* g = ws.get(gkey, gshape);
+    const HostW* be = bkey.empty() ? nullptr : ws.get(bkey, {K});
+    if (!g || (!bkey.empty() && !be) || p.size() != (size_t)O * K || base.cin != K) return f;
     std::vector<float> w(p.size()), cs(O), bias(O);
     for (int o = 0; o < O; ++o)
       for (int k = 0; k < K; ++k) w[(size_t)o * K + k] = p[(size_t)o * K + k] * g->v[k];
@@ -381,7 +384,7 @@ struct Packer {
       double c = 0, b = pb ? (*pb)[o] : 0.0;
       for (int k = 0; k < K; ++k) {
         c += C::dec(h[(size_t)o * K + k]);
-        b += (double)p[(size_t)o * K + k] * be->v[k];
+        if (be) b += (double)p[(size_t)o * K + k] * be->v[k];
       }
       cs[o] = (float)c;
       bias[o] = (float)b;
@@ -608,7 +611,8 @@ struct UNetNet {
   struct RB { ConvW c1, c2, res; bool has_res = false; int din = 0, dout = 0;
               const float* mw = nullptr; const float* mb = nullptr; int ss_off = 0; };
   struct LA { const float* gpre = nullptr; ConvW qkv; const float* wout = nullptr;
-              const float* bout = nullptr; const float* gout = nullptr; };
+              const float* bout = nullptr; const float* gout = nullptr;
+              ConvW qkv_f; const float* qkv_cs = nullptr; };   // PreNorm folded into to_qkv (C = 256)
   struct ST { const float* gpre = nullptr; const float *gnw = nullptr, *gnb = nullptr;
               ConvW pin; const float *n1w = nullptr, *n1b = nullptr, *n3w = nullptr, *n3b = nullptr;
               ConvW qkv, o, ff1, ff2, pout; const float *a2v = nullptr, *a2o = nullptr, *a2ob = nullptr;
@@ -669,7 +673,14 @@ struct UNetNet {
     const std::string f = p + "fn.fn.";
     if (!st) {
       a.la.gpre = P.f32(p + "fn.norm.g", {1, C, 1, 1});
-      a.la.qkv = P.conv(f + "to_qkv.weight", 384, C, 1, 1);
+      std::vector<float> pq;
+      a.la.qkv = P.conv(f + "to_qkv.weight", 384, C, 1, 1, "", false, 0, &pq);
+      if (sizeof(T) == 2 && !P.fp8 && !no_ln_fold() && C != 64 && C != 128) {
+        // The unfused LinearAttention path (C = 256): its channel LayerNorm (gain only) is
+        // folded into to_qkv like the SpatialTransformer's norm1.
+        auto fq = P.fold_ln(a.la.qkv, pq, 384, C, p + "fn.norm.g", "", nullptr, {1, C, 1, 1});
+        if (fq.cs) { a.la.qkv_f = fq.cw; a.la.qkv_cs = fq.cs; }
+      }
       a.la.wout = P.f32(f + "to_out.0.weight", {C, 128, 1, 1});
       a.la.bout = P.f32(f + "to_out.0.bias", {C});
       a.la.gout = P.f32(f + "to_out.1.g", {1, C, 1, 1});
@@ -869,10 +880,16 @@ struct UNetNet {
       emu_round<T>(r, y, C, M, C);
       return y;
     }
-    T* xn = r.alloc<T>(M * C);
-    ln<T>(r, x, C, xn, C, nullptr, 0, la.gpre, nullptr, (int)M, C, 1e-5f);
     T* qkv = r.alloc<T>(M * 384);
-    conv_call<T>(r, la.qkv, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 384, Epi());
+    if (la.qkv_cs && lnf_fits(C, 384, ACT_NONE, H * W)) {
+      Epi ef;                                       // PreNorm folded into to_qkv
+      ef.lnf_cs = la.qkv_cs; ef.lnf_n = C;
+      conv_call<T>(r, la.qkv_f, x, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 384, ef);
+    } else {
+      T* xn = r.alloc<T>(M * C);
+      ln<T>(r, x, C, xn, C, nullptr, 0, la.gpre, nullptr, (int)M, C, 1e-5f);
+      conv_call<T>(r, la.qkv, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, qkv, 384, Epi());
+    }
     // Context k v^T (MFMA) folded into per-image to_out weights (linattn.hip).
     T* weff = r.alloc<T>((size_t)B * C * 128);
     float* ws = r.alloc<float>(linear_attention_ws_floats(B, H * W));
@@ -929,7 +946,7 @@ struct UNetNet {
       Epi ep;
       ep.gna_stats = stats + (size_t)B * 32 * 32 * 3;
       ep.gna_g = s.gnw; ep.gna_b = s.gnb; ep.gna_groups = 32;
-      if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, r.st);
+      if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, B <= Run::kCounters ? r.counters : nullptr, r.st);
       conv_call<T>(r, s.pin, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, ep);
     } else {
       T* gn = r.alloc<T>(M * C);
@@ -1271,6 +1288,8 @@ class EngineT : public Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     zero_page = pool.alloc(256);
     HIP_OK(hipMemset(zero_page, 0, 256));
+    counters = (unsigned*)pool.alloc(Run::kCounters * sizeof(unsigned));
+    HIP_OK(hipMemset(counters, 0, Run::kCounters * sizeof(unsigned)));
     if (c.unet) unet = std::make_unique<UNetNet<T>>(c);
     if (c.vit) {
       if (c.image_size % c.patch_size || c.width % c.head_width || (c.head_width != 64 && c.head_width != 32) ||
@@ -1390,6 +1409,7 @@ class EngineT : public Engine {
     Run r;
     r.st = st;
     r.zero = zero_page;
+    r.counters = counters;
     r.dry = false;
     arena.dry = false;
     r.ar = &arena;
@@ -1603,6 +1623,7 @@ class EngineT : public Engine {
   hipEvent_t ev_in, ev_out;
   uint64_t noise_offset = 0;     // global index of image 0 (sharded runs)
   void* zero_page = nullptr;
+  unsigned* counters = nullptr;
 };
 
 std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {

@@ -106,6 +106,9 @@ struct Run {
   Arena* ar = nullptr;
   Profiler* prof = nullptr;
   const void* zero = nullptr;    // 256 zero bytes on the device (conv padding source)
+  // Zeroed device counters (kCounters); a kernel that counts in them puts them back to zero.
+  unsigned* counters = nullptr;
+  static constexpr int kCounters = 4096;
   double flops = 0;              // executed FLOPs (2*MAC) accumulated by the launches
   template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
 };

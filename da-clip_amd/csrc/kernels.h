@@ -80,9 +80,11 @@ bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
 // ... and a kernel applying the input GroupNorm in its A path (ConvArgs::gna_stats).
 bool conv_gna_ok(const ConvArgs& a, int elem_bytes);
 // GroupNorm statistics only (norm.hip): the (mean, rstd) table groupnorm() applies, at
-// part + B * groups * GN_CHUNKS * 3 (returned).
+// part + B * groups * GN_CHUNKS * 3 (returned). count: B zeroed device counters (left zeroed);
+// the last partial block of each image then merges it (one launch), else a gn_merge launch.
 template <typename T>
-const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part, hipStream_t st);
+const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part,
+                             unsigned* count, hipStream_t st);
 // The dispatcher can fuse a_w2/y2 into this 3x3 conv (bf16 v4 256x64 swapped-operand tiles).
 bool conv_res_fusable(const ConvArgs& a);
 

@@ -129,7 +129,8 @@ DEV Moments chan_merge(Moments a, Moments b) {
 
 template <typename T>
 __global__ void __launch_bounds__(256) gn_partial(const T* __restrict__ x, float* part, int HW,
-                                                  int C, int groups) {
+                                                  int C, int groups, unsigned* count = nullptr,
+                                                  float eps = 0.f) {
   constexpr int VE = TypeInfo<T>::VE;
   const int b = blockIdx.y, ch = blockIdx.x;
   const int NV = C / VE;                         // vectors per pixel (<= 256)
@@ -167,6 +168,28 @@ __global__ void __launch_bounds__(256) gn_partial(const T* __restrict__ x, float
     float* o = part + (((size_t)b * groups + g) * GN_CHUNKS + ch) * 3;
     o[0] = r.n; o[1] = r.mean; o[2] = r.m2;
   }
+  if (!count) return;
+  // Merge in the image's last chunk block (count[b] = chunk blocks done; the merging block puts
+  // it back to 0 for the next launch). Fixed merge order: identical to gn_merge's result.
+  __shared__ unsigned last;
+  __threadfence();                               // partials visible device-wide (all XCDs)
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(count + b, 1u) == GN_CHUNKS - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();                               // acquire the other blocks' partials
+  if ((int)threadIdx.x < groups) {
+    const int g = threadIdx.x;
+    const float* pp = part + ((size_t)b * groups + g) * GN_CHUNKS * 3;
+    Moments r{0.f, 0.f, 0.f};
+    for (int k = 0; k < GN_CHUNKS; ++k)
+      r = chan_merge(r, Moments{__builtin_nontemporal_load(pp + 3 * k), __builtin_nontemporal_load(pp + 3 * k + 1),
+                                __builtin_nontemporal_load(pp + 3 * k + 2)});
+    float* o = part + (size_t)gridDim.y * groups * GN_CHUNKS * 3 + ((size_t)b * groups + g) * 2;
+    o[0] = r.mean;
+    o[1] = 1.f / sqrtf(r.m2 / r.n + eps);
+  }
+  if (threadIdx.x == 0) atomicExch(count + b, 0u);
 }
 
 // Pass 2 (gn_merge): one thread per (image, group) merges its GN_CHUNKS partials in fixed
@@ -280,17 +303,22 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
 }
 
 template <typename T>
-const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part, hipStream_t st) {
+const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part,
+                             unsigned* count, hipStream_t st) {
   constexpr int VE = TypeInfo<T>::VE;
   const int NV = C / VE;
   if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64) abort();   // conv_gna_ok checks this
-  gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
-  gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
+  if (count) {
+    gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups, count, eps);
+  } else {
+    gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
+    gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
+  }
   return part + (size_t)B * groups * GN_CHUNKS * 3;
 }
 
 #define INST(T)                                                                              \
-  template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, hipStream_t); \
+  template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, unsigned*, hipStream_t); \
   template void layernorm<T>(const void*, int, void*, int, const void*, int, const float*,  \
                              const float*, int, int, float, hipStream_t);                   \
   template void groupnorm<T>(const void*, void*, const float*, const float*, int, int, int, \
