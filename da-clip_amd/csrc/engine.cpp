@@ -54,6 +54,12 @@ static bool no_ln_fold() {
   const char* e = getenv("DAC_NO_LN_FOLD");
   return e && atoi(e);
 }
+// DAC_NO_GN_IN_LN=1 (read per forward): GroupNorm statistics by their own pass (A/B aid).
+static bool no_gn_stats_in_ln() {
+  const char* e = getenv("DAC_NO_GN_IN_LN");
+  return e && atoi(e);
+}
+static unsigned dry_count = 0;   // stands in for the device counters in dry runs (never touched)
 static bool no_res_fuse() {
   static const int v = getenv("DAC_NO_RES_FUSE") ? atoi(getenv("DAC_NO_RES_FUSE")) : 0;
   return v != 0;
@@ -936,19 +942,29 @@ struct UNetNet {
     const int L = H * W;
     const size_t M = (size_t)B * L;
     T* xn = r.alloc<T>(M * C);
-    ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
     // GroupNorm workspace: partial moments [B][32 groups][GN_CHUNKS = 32][3], then the merged
-    // (mean, rstd) [B][32][2].
-    float* stats = r.alloc<float>((size_t)B * 32 * (32 * 3 + 2));
+    // (mean, rstd) [B][32][2]; or the PreNorm LN's per-block group sums + the table.
+    float* stats = r.alloc<float>(std::max((size_t)B * 32 * (32 * 3 + 2), layernorm_gnstats_ws_floats(B, L, 32)));
     T* hh = r.alloc<T>(M * C);
+    unsigned* cnt = B <= Run::kCounters ? r.counters : nullptr;
     if (gna_fits(C, C, L)) {
-      // proj_in reads xn and applies the GroupNorm to its A fragments (no normalised copy).
+      // proj_in reads xn and applies the GroupNorm to its A fragments (no normalised copy); the
+      // GroupNorm statistics come out of the PreNorm LayerNorm's own pass when it can take them.
+      const float* tab = (cnt || r.dry) && !no_gn_stats_in_ln()
+                             ? layernorm_gnstats<T>(x, C, xn, C, s.gpre, nullptr, (int)M, C, 1e-5f, L, 32, 1e-6f,
+                                                    stats, r.dry ? &dry_count : cnt, !r.dry, r.st)
+                             : nullptr;
+      if (!tab) {
+        ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
+        tab = stats + (size_t)B * 32 * 32 * 3;
+        if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, cnt, r.st);
+      }
       Epi ep;
-      ep.gna_stats = stats + (size_t)B * 32 * 32 * 3;
+      ep.gna_stats = tab;
       ep.gna_g = s.gnw; ep.gna_b = s.gnb; ep.gna_groups = 32;
-      if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, B <= Run::kCounters ? r.counters : nullptr, r.st);
       conv_call<T>(r, s.pin, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, ep);
     } else {
+      ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
       T* gn = r.alloc<T>(M * C);
       if (!r.dry) groupnorm<T>(xn, gn, s.gnw, s.gnb, B, L, C, 32, 1e-6f, stats, r.st);
       emu_round<T>(r, gn, C, M, C);

@@ -82,6 +82,14 @@ bool conv_gna_ok(const ConvArgs& a, int elem_bytes);
 // GroupNorm statistics only (norm.hip): the (mean, rstd) table groupnorm() applies, at
 // part + B * groups * GN_CHUNKS * 3 (returned). count: B zeroed device counters (left zeroed);
 // the last partial block of each image then merges it (one launch), else a gn_merge launch.
+// LayerNorm whose output also yields that tensor's GroupNorm statistics (norm.hip): returns the
+// (mean, rstd) table inside part, or nullptr if the shape is not covered; launch = false only
+// answers.
+template <typename T>
+const float* layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b,
+                               int rows, int C, float eps, int HW, int groups, float gn_eps, float* part,
+                               unsigned* count, bool launch, hipStream_t st);
+size_t layernorm_gnstats_ws_floats(int B, int HW, int groups);
 template <typename T>
 const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part,
                              unsigned* count, hipStream_t st);

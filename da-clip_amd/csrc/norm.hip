@@ -10,11 +10,19 @@
 
 namespace dac {
 
+// GroupNorm statistics of the LayerNorm OUTPUT, taken by the LayerNorm kernel itself (GNS):
+// the SpatialTransformer's PreNorm LN feeds its GroupNorm (attention.py:239-241), so the
+// GroupNorm's pass over the data is the LN's own. Per block (one image's RPB rows) plain sums
+// (sum y, sum y^2) per group, written in fixed order; the image's last block merges its
+// blocks' sums into (mean, rstd) (count[b]: zeroed counters, left zeroed).
+struct GnStats { float* part; unsigned* count; int HW, groups; float eps; };
+
 // G lanes per row (power of two), NVL 16-byte vectors per lane.
-template <typename T, int G, int NVL>
+template <typename T, int G, int NVL, bool GNS = false>
 __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ldx, T* y, int ldy,
                                                  const T* res, int ldr, const float* g,
-                                                 const float* b, int rows, int C, float eps) {
+                                                 const float* b, int rows, int C, float eps,
+                                                 GnStats gs = GnStats{}) {
   constexpr int VE = TypeInfo<T>::VE;
   const int lane = threadIdx.x & 63;
   const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / G) + lane / G;
@@ -56,10 +64,12 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
 #pragma unroll
   for (int o = G / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
   const float rstd = 1.f / sqrtf(q / (float)C + eps);
-  if (!live) return;
+  if (!GNS && !live) return;                     // (GNS: every row is live, see layernorm_gnstats)
+  float s1[NVL], s2[NVL];
 #pragma unroll
   for (int j = 0; j < NVL; ++j) {
     const int idx = sub + G * j;
+    s1[j] = s2[j] = 0.f;
     if (idx >= NV) continue;
     float o[VE];
 #pragma unroll
@@ -68,10 +78,91 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
       if (b) t += bv[j][e];
       if (res) t += rv[j][e];
       o[e] = t;
+      if constexpr (GNS) { s1[j] += t; s2[j] = fmaf(t, t, s2[j]); }
     }
     store_vec<T>(y + (size_t)row * ldy + idx * VE, o);
   }
+  if constexpr (GNS) {
+    // Group of vector idx = idx / vpg (vpg = vectors per group, divides G): sum the vpg lanes of
+    // a group, then the 64 / G rows of the wave; lanes sub % vpg == 0 of row 0 hold the sums.
+    const int vpg = C / gs.groups / VE;
+#pragma unroll
+    for (int j = 0; j < NVL; ++j) {
+      for (int o = 1; o < vpg; o <<= 1) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
+#pragma unroll
+      for (int o = G; o < 64; o <<= 1) { s1[j] += __shfl_xor(s1[j], o, 64); s2[j] += __shfl_xor(s2[j], o, 64); }
+    }
+    __shared__ float red[4][64][2];
+    const int wave = threadIdx.x >> 6;
+    if (lane < G && sub % vpg == 0) {
+#pragma unroll
+      for (int j = 0; j < NVL; ++j) {
+        const int idx = sub + G * j;
+        if (idx < NV) { red[wave][idx / vpg][0] = s1[j]; red[wave][idx / vpg][1] = s2[j]; }
+      }
+    }
+    __syncthreads();
+    constexpr int RPB = 4 * (64 / G);
+    const int nb = gs.HW / RPB;                  // blocks per image
+    const int img = (int)((long)blockIdx.x * RPB / gs.HW), blk = blockIdx.x - img * nb;
+    const int t = threadIdx.x;
+    if (t < gs.groups) {
+      const float a0 = red[0][t][0] + red[1][t][0] + red[2][t][0] + red[3][t][0];
+      const float a1 = red[0][t][1] + red[1][t][1] + red[2][t][1] + red[3][t][1];
+      float* o = gs.part + (((size_t)img * gs.groups + t) * nb + blk) * 2;
+      o[0] = a0; o[1] = a1;
+    }
+    __shared__ unsigned last;
+    __threadfence();                             // block sums visible device-wide (all XCDs)
+    __syncthreads();
+    if (t == 0) last = atomicAdd(gs.count + img, 1u) == (unsigned)nb - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();                             // acquire the other blocks' sums
+    if (t < gs.groups) {
+      const float* pp = gs.part + ((size_t)img * gs.groups + t) * nb * 2;
+      float a0 = 0.f, a1 = 0.f;
+      for (int k = 0; k < nb; ++k) { a0 += __builtin_nontemporal_load(pp + 2 * k); a1 += __builtin_nontemporal_load(pp + 2 * k + 1); }
+      const float n = (float)gs.HW * (float)(C / gs.groups);
+      const float mu = a0 / n, var = fmaxf(a1 / n - mu * mu, 0.f);
+      float* o = gs.part + (size_t)(rows / gs.HW) * gs.groups * nb * 2 + ((size_t)img * gs.groups + t) * 2;
+      o[0] = mu;
+      o[1] = 1.f / sqrtf(var + gs.eps);
+    }
+    if (t == 0) atomicExch(gs.count + img, 0u);
+  }
 }
+
+// LayerNorm (gain, bias) whose output also yields the GroupNorm(groups) statistics; 16-bit rows
+// of 256 or 512 channels (the SpatialTransformer widths), HW a multiple of the block's rows.
+// Returns the (mean, rstd) table, at part + (rows / HW) * groups * nb * 2, or nullptr when the
+// shape is not covered (the caller then runs layernorm + groupnorm_stats). launch = false only
+// answers (the engine's dry run).
+template <typename T>
+const float* layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b,
+                               int rows, int C, float eps, int HW, int groups, float gn_eps, float* part,
+                               unsigned* count, bool launch, hipStream_t st) {
+  constexpr int VE = TypeInfo<T>::VE;
+  const int NV = C / VE;
+#define LNG(G, NVL)                                                                                 \
+  {                                                                                                 \
+    constexpr int RPB = 4 * (64 / G);                                                               \
+    const int vpg = groups > 0 && C % groups == 0 ? C / groups / VE : 0;                            \
+    if (vpg < 1 || G % vpg || (C / groups) % VE || HW % RPB || rows % HW || groups > 64 || !count)  \
+      return nullptr;                                                                               \
+    if (launch)                                                                                     \
+      ln_kernel<T, G, NVL, true><<<rows / RPB, 256, 0, st>>>((const T*)x, ldx, (T*)y, ldy, nullptr, \
+                                                             0, g, b, rows, C, eps,                 \
+                                                             GnStats{part, count, HW, groups, gn_eps}); \
+    return part + (size_t)(rows / HW) * groups * (HW / RPB) * 2;                                    \
+  }
+  if (sizeof(T) == 2 && NV == 32) LNG(8, 4)
+  if (sizeof(T) == 2 && NV == 64) LNG(16, 4)
+#undef LNG
+  return nullptr;
+}
+// Workspace floats of layernorm_gnstats (block sums + the table), an upper bound.
+size_t layernorm_gnstats_ws_floats(int B, int HW, int groups) { return (size_t)B * groups * (2 * (HW / 16) + 2); }
 
 template <typename T>
 void layernorm(const void* x, int ldx, void* y, int ldy, const void* res, int ldr,
@@ -319,6 +410,8 @@ const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, fl
 
 #define INST(T)                                                                              \
   template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, unsigned*, hipStream_t); \
+  template const float* layernorm_gnstats<T>(const void*, int, void*, int, const float*, const float*, int, int, \
+                                             float, int, int, float, float*, unsigned*, bool, hipStream_t); \
   template void layernorm<T>(const void*, int, void*, int, const void*, int, const float*,  \
                              const float*, int, int, float, hipStream_t);                   \
   template void groupnorm<T>(const void*, void*, const float*, const float*, int, int, int, \
