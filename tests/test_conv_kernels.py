@@ -31,15 +31,32 @@ def test_conv3x3_kernels_match_naive_reference():
 
 
 @pytest.mark.gpu
-def test_ln_folded_gemms_match_host_reference():
+def test_norm_folded_gemms_match_host_reference():
     """SpatialTransformer norm1 -> q|k|v and norm3 -> GEGLU proj as ONE GEMM each (EPI_LNF: the
     LN gain folded into the weights, the row moments taken from the kernel's own A fragments,
     engine.cpp Packer::fold_ln) against a host fp64 LayerNorm + GEMM (+ GEGLU) with the exact
-    weights, on rows offset by several standard deviations (attention.py:253-261; LN eps 1e-5).
-    Bound 1e-2 max-rel: bf16 operands and output (measured figures in the printout)."""
+    weights, on rows offset by several standard deviations (attention.py:253-261; LN eps 1e-5);
+    and proj_in with the GroupNorm(32, eps 1e-6) applied to its A fragments (EPI_GNA) against a
+    host GroupNorm + GEMM (attention.py:76-77, 239-241). Bound 1e-2 max-rel: bf16 operands and
+    output (measured figures in the printout)."""
     assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
     out = subprocess.run([BIN, "lnf", "3"], capture_output=True, text=True, timeout=300, cwd=ROOT)
     print(out.stdout)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check rel" in l]
     assert len(rows) == 6 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+
+
+@pytest.mark.gpu
+def test_prenorm_layernorm_groupnorm_stats():
+    """The SpatialTransformer's PreNorm LayerNorm kernel also produces the GroupNorm(32) statistics
+    of its output (norm.hip layernorm_gnstats: per-block group sums, merged by each image's last
+    block through zeroed device counters), so proj_in applies the GroupNorm in its A path with no
+    separate pass (attention.py:76-77, 239-241). Against host fp64: xn rel < 1e-2 (bf16 output),
+    GroupNorm mean abs < 1e-4 and rstd rel < 1e-4; run twice, counters back at zero."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "gns"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l for l in out.stdout.splitlines() if "check" in l]
+    assert len(rows) == 4 and all(l.rstrip().endswith("OK") for l in rows), out.stdout

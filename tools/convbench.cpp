@@ -389,8 +389,82 @@ static int lnf_check(int iters) {
   return fails;
 }
 
+// PreNorm LayerNorm with the GroupNorm statistics of its output (norm.hip layernorm_gnstats):
+// xn against a host LayerNorm (gain only, eps 1e-5) and the (mean, rstd) table against host
+// GroupNorm(32, eps 1e-6) moments of the host LayerNorm output; run twice (the per-image counters
+// must come back to zero).
+static int gns_check() {
+  int fails = 0;
+  for (int C : {512, 256}) {
+    const int B = 8, HW = 1024, M = B * HW, G = 32, cpg = C / G;
+    uint32_t h = 99 + C;
+    auto rnd = [&]() { h = h * 1664525u + 1013904223u; return ((h >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb((size_t)M * C);
+    std::vector<float> g(C);
+    for (int c = 0; c < C; ++c) g[c] = 1.f + 0.8f * rnd();
+    for (int m = 0; m < M; ++m) {
+      const float off = 3.f * rnd();
+      for (int c = 0; c < C; ++c) xb[(size_t)m * C + c] = (bf16)(off + (1.f + 0.3f * std::sin(0.05f * c)) * rnd() + 0.2f * std::cos(0.7f * c));
+    }
+    std::vector<double> ln((size_t)M * C);
+    for (int m = 0; m < M; ++m) {
+      double mu = 0, var = 0;
+      for (int c = 0; c < C; ++c) mu += bf2f(xb[(size_t)m * C + c]);
+      mu /= C;
+      for (int c = 0; c < C; ++c) { const double d = bf2f(xb[(size_t)m * C + c]) - mu; var += d * d; }
+      const double rs = 1.0 / std::sqrt(var / C + 1e-5);
+      for (int c = 0; c < C; ++c) ln[(size_t)m * C + c] = (bf2f(xb[(size_t)m * C + c]) - mu) * rs * g[c];
+    }
+    std::vector<double> st((size_t)B * G * 2);
+    for (int b = 0; b < B; ++b)
+      for (int gi = 0; gi < G; ++gi) {
+        double s1 = 0, s2 = 0;
+        for (int p = 0; p < HW; ++p)
+          for (int c = gi * cpg; c < (gi + 1) * cpg; ++c) s1 += ln[((size_t)b * HW + p) * C + c];
+        const double mu = s1 / (HW * cpg);
+        for (int p = 0; p < HW; ++p)
+          for (int c = gi * cpg; c < (gi + 1) * cpg; ++c) { const double d = ln[((size_t)b * HW + p) * C + c] - mu; s2 += d * d; }
+        st[((size_t)b * G + gi) * 2] = mu;
+        st[((size_t)b * G + gi) * 2 + 1] = 1.0 / std::sqrt(s2 / (HW * cpg) + 1e-6);
+      }
+    void *dx, *dy; float *dg, *dpart; unsigned* dcnt;
+    const size_t wsf = layernorm_gnstats_ws_floats(B, HW, G);
+    CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dy, xb.size() * 2)); CK(hipMalloc(&dg, C * 4));
+    CK(hipMalloc(&dpart, wsf * 4)); CK(hipMalloc(&dcnt, B * 4)); CK(hipMemset(dcnt, 0, B * 4));
+    CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, g.data(), C * 4, hipMemcpyHostToDevice));
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipMemset(dpart, 0xff, wsf * 4));
+      const float* tab = layernorm_gnstats<bf16>(dx, C, dy, C, dg, nullptr, M, C, 1e-5f, HW, G, 1e-6f, dpart, dcnt, true, 0);
+      if (!tab) { printf("gns C=%d not eligible\n", C); ++fails; break; }
+      CK(hipDeviceSynchronize());
+      std::vector<bf16> yb(xb.size());
+      std::vector<float> tb(st.size());
+      std::vector<unsigned> cnt(B);
+      CK(hipMemcpy(yb.data(), dy, yb.size() * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(tb.data(), tab, tb.size() * 4, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(cnt.data(), dcnt, B * 4, hipMemcpyDeviceToHost));
+      double ey = 0, my = 0, em = 0, er = 0;
+      for (size_t i = 0; i < yb.size(); ++i) { ey = std::max(ey, std::fabs(bf2f(yb[i]) - ln[i])); my = std::max(my, std::fabs(ln[i])); }
+      for (int i = 0; i < B * G; ++i) {
+        em = std::max(em, std::fabs(tb[2 * i] - st[2 * i]));
+        er = std::max(er, std::fabs(tb[2 * i + 1] - st[2 * i + 1]) / st[2 * i + 1]);
+      }
+      unsigned cz = 0;
+      for (unsigned c : cnt) cz |= c;
+      const bool ok = ey / my < 1e-2 && em < 1e-4 && er < 1e-4 && cz == 0;
+      printf("gns C=%d rep %d: xn rel %.2e, mean abs %.2e, rstd rel %.2e, counters %s  check %s\n", C, rep, ey / my,
+             em, er, cz ? "NOT ZERO" : "zero", ok ? "OK" : "FAIL");
+      fails += !ok;
+    }
+    CK(hipFree(dx)); CK(hipFree(dy)); CK(hipFree(dg)); CK(hipFree(dpart)); CK(hipFree(dcnt));
+  }
+  return fails;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
+  if (argc > 1 && !strcmp(argv[1], "gns")) return gns_check();
   if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
   int iters = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 && argv[2][0] ? argv[2] : nullptr;   // substring filter
