@@ -186,7 +186,7 @@ bool conv8_ok(const ConvArgs& a, int kh, int kw, int s, int p) {
   const bool shape = (kh == 3 && kw == 3 && s == 1 && p == 1) || (kh == 1 && kw == 1 && s == 1 && p == 0) ||
                      (kh == 4 && kw == 4 && s == 2 && p == 1);
   return shape && a.zero && a.Cin % 64 == 0 && (a.x2 == nullptr || a.C1 % 64 == 0) && a.amode == 0 &&
-         a.w_bstride == 0 && !a.ln_g && !a.lnf_cs && a.cwrap == 0 && a.Cout >= 32 && (kh > 1 || a.up == 0);
+         a.w_bstride == 0 && !a.ln_g && !a.lnf_cs && !a.gna_stats && a.cwrap == 0 && a.Cout >= 32 && (kh > 1 || a.up == 0);
 }
 
 void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, const uint8_t* ws8, int Kp,
