@@ -381,6 +381,162 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
   }
 }
 
+// ------------------------------------------------------------------ K/V-ring variant
+// flash_kr_kernel (bf16 / f16, L % 64 == 0): the same transposed MFMA formulation and LDS image
+// as flash_kv, but K / V stream through a 3-slot ring of 64-key chunks (8 KB a slot, 24 KB a
+// block) instead of being resident (128 KB), and a block is 4 waves x QG x 16 queries. Four
+// blocks then share a CU (16 waves, against flash_kv's 8), so one wave's S -> max -> exp -> PV
+// chain overlaps other waves' MFMAs. Each chunk is one barrier: at chunk c the slot of chunk c-1
+// (read by every wave before that barrier) is refilled with chunk c+2.
+constexpr int FKR_NW = 4, FKR_NST = 3, FKR_CK = 64;
+template <typename T, int QG>
+__global__ void __launch_bounds__(64 * FKR_NW) flash_kr_kernel(const T* __restrict__ qkv, T* o, int L,
+                                                              int H, float scale) {
+  constexpr int D = 32, SLOT = FKR_CK * 64;          // bytes of one K (or V) chunk
+  __shared__ __attribute__((aligned(1024))) char smem[2 * FKR_NST * SLOT];
+  char* sK = smem;
+  char* sV = smem + FKR_NST * SLOT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int gx = gridDim.x, gy = gridDim.y, n = gx * gy * gridDim.z;
+  const int id = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int xq = n / 8, xr = n % 8, xcd = id % 8;
+  const int t = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + id / 8;
+  const int bx = t % gx, h = (t / gx) % gy, b = t / (gx * gy);
+  const int ld = 3 * H * D;
+  const T* base = qkv + (size_t)b * L * ld;
+
+  u32x4 qf[QG];
+  int qi[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    qi[g] = bx * (FKR_NW * 16 * QG) + wave * (16 * QG) + g * 16 + lr;
+    qf[g] = *reinterpret_cast<const u32x4*>(base + (size_t)qi[g] * ld + h * D + lg * 8);
+  }
+  // Chunk c -> slot c % NST: wave w fills keys 16w .. 16w+15 of the chunk, of K and of V.
+  const int NC = L / FKR_CK;
+  auto issue = [&](int c) {
+    const int kl = 16 * wave + (lane >> 2), ch = lane & 3;
+    const T* src = base + (size_t)(c * FKR_CK + kl) * ld + h * D + 8 * (ch ^ fkv_swz(kl));
+    char* dk = sK + (c % FKR_NST) * SLOT + wave * 1024;
+    char* dv = sV + (c % FKR_NST) * SLOT + wave * 1024;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + H * D),
+                                     (__attribute__((address_space(3))) void*)dk, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * H * D),
+                                     (__attribute__((address_space(3))) void*)dv, 16, 0, 0);
+  };
+#pragma unroll
+  for (int c = 0; c < FKR_NST - 1; ++c)
+    if (c < NC) issue(c);
+
+  f32x4 oacc[QG][2], lacc[QG];
+  float mrun[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    oacc[g][0] = oacc[g][1] = lacc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mrun[g] = -INFINITY;
+  }
+  const uint32_t one2 = std::is_same<T, f16>::value ? 0x3C003C00u : 0x3F803F80u;
+  const u32x4 ones = u32x4{one2, one2, one2, one2};
+  const float cs = scale * 1.4426950408889634f;
+  typedef short v4i16 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+  for (int c = 0; c < NC; ++c) {
+    // This wave's DMAs of chunk c landed (the chunks issued after it may stay in flight), then
+    // every wave's; after the barrier no wave still reads chunk c-1's slot.
+    const int younger = NC - 1 - c < FKR_NST - 2 ? NC - 1 - c : FKR_NST - 2;
+    fkv_wait<2 * (FKR_NST - 2)>(2 * younger);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + FKR_NST - 1 < NC) issue(c + FKR_NST - 1);
+    const char* k0 = sK + (c % FKR_NST) * SLOT;
+    const char* v0 = sV + (c % FKR_NST) * SLOT;
+    u32x4 kf[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int key = mi * 16 + lr;
+      kf[mi] = *reinterpret_cast<const u32x4*>(k0 + key * 64 + ((lg ^ fkv_swz(key)) << 4));
+    }
+    u32x4 vf[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int dm = 0; dm < 2; ++dm) {
+        uint32_t w[4];
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi) {
+          const int key = 32 * st + 16 * hi + 4 * lg + (lr >> 2);
+          const int byte = (dm * 16 + 4 * (lr & 3)) * 2;
+          const int off = key * 64 + ((((byte >> 4) ^ fkv_swz(key)) << 4) | (byte & 15));
+          const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(v0 + off));
+          const uint2 u = __builtin_bit_cast(uint2, r);
+          w[2 * hi] = u.x;
+          w[2 * hi + 1] = u.y;
+        }
+        vf[st][dm] = u32x4{w[0], w[1], w[2], w[3]};
+      }
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      f32x4 s[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        s[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        Mma<T>::run(s[mi], kf[mi], qf[g]);
+      }
+      float tmax = s[0][0];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[mi][r]);
+      tmax = red16_max(tmax);
+      tmax = red32_max(tmax);
+      const float mnew = fmaxf(mrun[g], tmax * cs);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
+      if (DAC_FKV_SKIP == 0 || __any(mnew != mrun[g])) {
+        const float corr = __builtin_amdgcn_exp2f(mrun[g] - mnew);
+        lacc[g] *= corr;
+#pragma unroll
+        for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+      }
+      mrun[g] = mnew;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        typename Vec8<T>::t pb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[j] = (T)s[2 * st][j];
+          pb[4 + j] = (T)s[2 * st + 1][j];
+        }
+        const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
+#pragma unroll
+        for (int dm = 0; dm < 2; ++dm) Mma<T>::run(oacc[g][dm], vf[st][dm], pbu);
+        Mma<T>::run(lacc[g], ones, pbu);
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    const float inv = 1.f / lacc[g][0];
+    T* out = o + ((size_t)b * L + qi[g]) * (H * D) + h * D;
+#pragma unroll
+    for (int dm = 0; dm < 2; ++dm) {
+      typename Vec8<T>::t2 v0, v1;
+      v0[0] = (T)(oacc[g][dm][0] * inv); v0[1] = (T)(oacc[g][dm][1] * inv);
+      v1[0] = (T)(oacc[g][dm][2] * inv); v1[1] = (T)(oacc[g][dm][3] * inv);
+      uint2 stv;
+      stv.x = __builtin_bit_cast(uint32_t, v0);
+      stv.y = __builtin_bit_cast(uint32_t, v1);
+      *reinterpret_cast<uint2*>(out + dm * 16 + 4 * lg) = stv;
+    }
+  }
+}
+// 1: the K/V-ring kernel is the dispatcher's choice for the L <= 1024 shapes (DAC_FLASH_KR).
+int g_flash_kr = getenv("DAC_FLASH_KR") ? atoi(getenv("DAC_FLASH_KR")) : 0;
+
 template <typename T, int QG>
 static void fkv_optin() {
   // > 64 KB of dynamic LDS must be opted into, once per (kernel, device).
@@ -394,11 +550,24 @@ static void fkv_optin() {
 }
 
 // variant: 0 = the dispatcher's choice (g_flash_old = DAC_FLASH_OLD selects the staged-tile
-// kernel process-wide), 1 = the staged-tile kernel. Passed explicitly by the op-level test
+// kernel process-wide, g_flash_kr = DAC_FLASH_KR the K/V-ring one), 1 = the staged-tile kernel,
+// 2 = the K/V-ring kernel (16-bit, L % 64 == 0). Passed explicitly by the op-level test
 // hook, so no global state is toggled per call.
 template <typename T>
 void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale, int variant, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    if (L % 64 == 0 && (variant == 2 || (variant == 0 && g_flash_kr && !g_flash_old && L % 128 == 0 && L <= 1024))) {
+      // K/V-ring kernel: 2 query groups per wave (128 queries per block) while that leaves
+      // >= 1024 blocks (4 per CU), else 1.
+      if (L % 128 == 0 && (long)(L / 128) * H * B >= 1024) {
+        dim3 g(L / 128, H, B);
+        flash_kr_kernel<T, 2><<<g, 64 * FKR_NW, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+      } else {
+        dim3 g(L / 64, H, B);
+        flash_kr_kernel<T, 1><<<g, 64 * FKR_NW, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
+      }
+      return;
+    }
     if (L % 128 == 0 && L <= 1024 && variant == 0 && !g_flash_old) {
       // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
       // fills the chip, else 2 (or 1).

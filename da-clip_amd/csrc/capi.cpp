@@ -281,7 +281,8 @@ double dac_encode_flops(dac_handle* h, int B) {
 int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype, int variant,
                      void* stream) {
   if (!qkv || !out || B <= 0 || L <= 0 || H <= 0 ||
-      (dtype != DAC_F32 && dtype != DAC_BF16 && dtype != DAC_F16) || variant < 0 || variant > 1)
+      (dtype != DAC_F32 && dtype != DAC_BF16 && dtype != DAC_F16) || variant < 0 || variant > 2 ||
+      (variant == 2 && (dtype == DAC_F32 || L % 64)))
     return DAC_E_ARG;
   const float scale = 1.f / std::sqrt(32.f);
   const hipStream_t st = (hipStream_t)stream;

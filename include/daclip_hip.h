@@ -173,7 +173,8 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
 /* Op-level test hook: the SpatialTransformer self-attention core on its own (the kernel
  * dac_unet_forward runs for attention.py:170-193). qkv is [B*L, 3*H*32] (q | k | v, heads
  * of 32), out [B*L, H*32], both in `dtype` (DAC_F32 / DAC_BF16) on the current device;
- * scale = 32^-0.5. variant: 0 = the dispatcher's choice, 1 = the staged-tile kernel.
+ * scale = 32^-0.5. variant: 0 = the dispatcher's choice, 1 = the staged-tile kernel,
+ * 2 = the K/V-ring kernel (16-bit dtypes, L % 64 == 0; DAC_E_ARG otherwise).
  * dtype: DAC_F32, DAC_BF16 or DAC_F16. */
 int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype, int variant,
                      void* stream);

@@ -3,8 +3,8 @@ heads of d = 32, softmax(q k^T * 32^-0.5) v) through the C ABI hook dac_op_atten
 a plain PyTorch fp32 reference of the same op on the same bf16 / fp16 (or fp32) inputs.
 
 Covers the K/V-resident kernel (bf16, L % 128 == 0, L <= 1024: the 32x32 UNet levels at 256^2)
-in each of its query-group configurations, the staged-tile kernel it falls back to (ragged L,
-fp32, or forced), and that the two agree."""
+in each of its query-group configurations, the K/V-ring kernel (variant 2, L % 64 == 0), the
+staged-tile kernel it falls back to (ragged L, fp32, or forced), and that they agree."""
 import ctypes
 
 import pytest
@@ -44,7 +44,7 @@ def test_attention_16bit_matches_fp32_reference(B, L, H, dt):
     tdt, code = (torch.bfloat16, _lib.DAC_BF16) if dt == "bf16" else (torch.float16, _lib.DAC_F16)
     qkv = (torch.randn(B * L, 3 * H * 32, device="cuda", generator=g) * 1.5).to(tdt)
     ref = _ref(qkv, B, L, H)
-    for variant in (0, 1):
+    for variant in ((0, 1, 2) if L % 64 == 0 else (0, 1)):
         out = _run(qkv, B, L, H, code, variant).float()
         err = (out - ref).abs().max().item() / ref.abs().max().item()
         # 16-bit P and output rounding: measured ~3e-3 (bf16); fp16 8x finer.
@@ -64,9 +64,11 @@ def test_attention_kernels_agree_and_handle_peaky_scores():
     ref = _ref(qkv, B, L, H)
     a = _run(qkv, B, L, H, _lib.DAC_BF16, 0).float()
     b = _run(qkv, B, L, H, _lib.DAC_BF16, 1).float()
-    assert torch.isfinite(a).all()
+    c = _run(qkv, B, L, H, _lib.DAC_BF16, 2).float()
+    assert torch.isfinite(a).all() and torch.isfinite(c).all()
     assert (a - ref).abs().max().item() / ref.abs().max().item() < 1e-2
     assert (a - b).abs().max().item() / ref.abs().max().item() < 1e-2
+    assert (c - ref).abs().max().item() / ref.abs().max().item() < 1e-2
 
 
 def test_attention_fp32_matches_reference():

@@ -15,7 +15,7 @@ st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 for (B, L, H) in [(8, 1024, 16), (8, 1024, 8)]:
     qkv = torch.randn(B * L, 3 * H * 32, device="cuda").to(torch.bfloat16)
     out = torch.empty(B * L, H * 32, device="cuda", dtype=torch.bfloat16)
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         args = (ctypes.c_void_p(qkv.data_ptr()), ctypes.c_void_p(out.data_ptr()), B, L, H, _lib.DAC_BF16, variant, st)
         for _ in range(3):
             L_.dac_op_attention(*args)
