@@ -48,16 +48,21 @@ static int key_role(const std::string& k) {
 template <typename T>
 static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
 // DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
+// Norm folding (LN into q|k|v / GEGLU / to_qkv, GroupNorm into proj_in's A path, GroupNorm
+// statistics from the PreNorm LayerNorm) on by default once validated on the GPU.
+constexpr bool kNormFoldDefault = false;
 // DAC_NO_LN_FOLD=1 (read when a handle's weights are packed): SpatialTransformer norm1 / norm3
 // as separate LayerNorm launches (A/B aid; tests/test_lnfold.py).
 static bool no_ln_fold() {
   const char* e = getenv("DAC_NO_LN_FOLD");
-  return e && atoi(e);
+  if (e) return atoi(e) != 0;
+  return !kNormFoldDefault;
 }
 // DAC_NO_GN_IN_LN=1 (read per forward): GroupNorm statistics by their own pass (A/B aid).
 static bool no_gn_stats_in_ln() {
   const char* e = getenv("DAC_NO_GN_IN_LN");
-  return e && atoi(e);
+  if (e) return atoi(e) != 0;
+  return !kNormFoldDefault;
 }
 static unsigned dry_count = 0;   // stands in for the device counters in dry runs (never touched)
 static bool no_res_fuse() {
