@@ -1540,13 +1540,22 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 // Kernel shape of the 64 -> 64 3x3 convs: DAC_C3W=<waves>,<TM>,<stages> (tuning), default
 // 8 waves x 64-pixel segments x 2 stages.
 struct C3WCfg { int nwv = 8, tm = 4, nst = 2; };
-inline C3WCfg c3w_cfg() {
+// Small grids (fewer 64-pixel segments than two per wave of a full-chip launch: the 128x128
+// level) may take another shape (DAC_C3W_SMALL); DAC_C3W forces one shape everywhere.
+constexpr C3WCfg kC3WSmall{8, 4, 2};
+inline C3WCfg c3w_cfg(bool small = false) {
   static C3WCfg c = [] {
     C3WCfg r;
     if (const char* e = getenv("DAC_C3W")) sscanf(e, "%d,%d,%d", &r.nwv, &r.tm, &r.nst);
     return r;
   }();
-  return c;
+  static C3WCfg cs = [] {
+    C3WCfg r = kC3WSmall;
+    if (const char* e = getenv("DAC_C3W")) sscanf(e, "%d,%d,%d", &r.nwv, &r.tm, &r.nst);
+    else if (const char* e2 = getenv("DAC_C3W_SMALL")) sscanf(e2, "%d,%d,%d", &r.nwv, &r.tm, &r.nst);
+    return r;
+  }();
+  return small ? cs : c;
 }
 inline int conv3w_blocks(int ntiles, int nwv) {
   static int ncu = 0;
@@ -1562,7 +1571,7 @@ inline int conv3w_blocks(int ntiles, int nwv) {
 }
 template <typename T>
 void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
-  const C3WCfg c = c3w_cfg();
+  const C3WCfg c = c3w_cfg(a.Wo % 64 == 0 && (long)a.B * a.Ho * (a.Wo / 64) < 2L * 256 * C3W_WAVES);
 #define DAC_C3W(NW_, TM_, NS_)                                                                 \
   if (c.nwv == NW_ && c.tm == TM_ && c.nst == NS_ && a.Wo % (16 * TM_) == 0) {                  \
     const int ntiles = a.B * a.Ho * (a.Wo / (16 * TM_));                                        \
