@@ -3,7 +3,9 @@
 tools/convbench (built in-tree by __graft_entry__.build) runs every UNet 3x3 shape through each
 kernel choice on random inputs and compares the full output with a naive one-thread-per-output
 fp32 conv of the same bf16 operands and the same epilogue (bias, per-image scale/shift, SiLU,
-residual): max |diff| / max |ref| < 1e-2. Choices: -1 built-in (v5 weight-stationary for
+residual): max |diff| / max |ref| < 1e-2; and, independently of any GPU code, 2048 sampled
+outputs per shape against a host fp64 recomputation from the operands copied back ("host rel",
+same bound). Choices: -1 built-in (v5 weight-stationary for
 64 -> 64, swapped-epilogue v4 elsewhere), 18 v4 LDS epilogue, 40 / 41 swapped v4 256x64 /
 128x64, 20 v4 128x64, 30 v5 without the SIMD-partner offset, 0 v3."""
 import os

@@ -563,7 +563,48 @@ int main(int argc, char** argv) {
         md = fmax(md, fabs((double)(float)yh[yi] - r[i]));
         mx = fmax(mx, fabs((double)r[i]));
       }
-      printf("  check rel %.2e %s", md / mx, md / mx < 1e-2 ? "OK" : "FAIL");
+      // Independent host (fp64) reference at 2048 sampled outputs: the operands are copied back
+      // and the conv + epilogue recomputed on the CPU (the naive reference above is GPU code).
+      double hd = 0, hm = 0;
+      if (s.act != 3) {
+        const size_t nx = (size_t)s.B * s.H * s.W * s.cin, nw = (size_t)s.cout * a.K;
+        std::vector<bf16> hx(nx), hw(nw), hr(s.res ? n : 0);
+        std::vector<float> hss(s.ss ? (size_t)s.B * 2 * s.cout : 0), hb(s.bias ? s.cout : 0);
+        CK(hipMemcpy(hx.data(), x, nx * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hw.data(), w, nw * 2, hipMemcpyDeviceToHost));
+        if (s.res) CK(hipMemcpy(hr.data(), res, n * 2, hipMemcpyDeviceToHost));
+        if (s.ss) CK(hipMemcpy(hss.data(), ss, hss.size() * 4, hipMemcpyDeviceToHost));
+        if (s.bias) CK(hipMemcpy(hb.data(), bias, hb.size() * 4, hipMemcpyDeviceToHost));
+        uint32_t st = 12345u + (uint32_t)n;
+        for (int q = 0; q < 2048; ++q) {
+          st = st * 1664525u + 1013904223u;
+          const size_t i = ((size_t)st * 2654435761u) % n;
+          const int nn = (int)(i % s.cout);
+          const size_t m = i / s.cout;
+          const int b = (int)(m / ((size_t)a.Ho * a.Wo)), rr = (int)(m % ((size_t)a.Ho * a.Wo));
+          const int oh = rr / a.Wo, ow = rr % a.Wo;
+          double acc = 0;
+          for (int y0 = 0; y0 < s.kh; ++y0)
+            for (int z0 = 0; z0 < s.kh; ++z0) {
+              const int ih = oh * s.s - s.p + y0, iw = ow * s.s - s.p + z0;
+              const int Hin = s.up ? 2 * s.H : s.H, Win = s.up ? 2 * s.W : s.W;
+              if (ih < 0 || iw < 0 || ih >= Hin || iw >= Win) continue;
+              const int sh = s.up ? ih >> 1 : ih, sw = s.up ? iw >> 1 : iw;
+              const bf16* xp = &hx[((size_t)(b * s.H + sh) * s.W + sw) * s.cin];
+              const bf16* wp = &hw[(((size_t)nn * s.kh + y0) * kws + z0) * s.cin];
+              for (int c = 0; c < s.cin; ++c) acc += (double)bf2f(xp[c]) * bf2f(wp[c]);
+            }
+          if (s.bias) acc += hb[nn];
+          if (s.ss) acc = acc * (hss[(size_t)b * 2 * s.cout + nn] + 1.0) + hss[(size_t)b * 2 * s.cout + s.cout + nn];
+          if (s.act == 1) acc = acc / (1.0 + std::exp(-acc));
+          if (s.res) acc += bf2f(hr[m * s.cout + nn]);
+          const double got = (float)yh[m * a.ldy + nn];
+          hd = fmax(hd, fabs(got - acc));
+          hm = fmax(hm, fabs(acc));
+        }
+      }
+      const bool hok = s.act == 3 || hd / hm < 1e-2;
+      printf("  host rel %.2e  check rel %.2e %s", hm > 0 ? hd / hm : 0.0, md / mx, md / mx < 1e-2 && hok ? "OK" : "FAIL");
     }
     printf("\n");
   }
