@@ -10,7 +10,6 @@ int g_conv2_force = 0;
 // Tuning aid: DAC_CONV2_FORCE32=k forces 1x1 configuration k on the small-image GEMMs only
 // (Ho*Wo <= 1024: the SpatialTransformer level), for in-network sweeps.
 int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
-int g_conv3_stagger = getenv("DAC_V4_STAGGER") ? atoi(getenv("DAC_V4_STAGGER")) : 0;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
 extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }

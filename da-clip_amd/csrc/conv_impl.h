@@ -931,15 +931,6 @@ conv3i_kernel(ConvArgs a, int RW) {
   using SA = RowSwz<SLOTS, TM>;
   using SB = RowSwz<SLOTS, 1>;
 
-  if (a.stagger) {
-    // First-round blocks [slots/2, slots) (slots = 2 per CU): the dispatcher deals an XCD's
-    // blocks over its CUs in turn, so block j and j + slots/2 share a CU.
-    // (stagger < 0: the alternative pairing, XCD-local neighbours j, j + 1.)
-    const int id = blockIdx.x + gridDim.x * blockIdx.y;
-    const int n = a.stagger > 0 ? a.stagger : -a.stagger;
-    if (a.stagger > 0 ? (id >= 256 && id < 512) : (id < 512 && ((id >> 3) & 1)))
-      for (int k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(32);
-  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform in an SGPR
   const int wm = wave / WGN, wn = wave % WGN;
@@ -1278,7 +1269,6 @@ extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 extern int g_conv3_buf;       // v4 buffer-resource DMA (FL bit 10); DAC_CONV3_BUF=0 disables
-extern int g_conv3_stagger;   // v4 first-round stagger (ConvArgs::stagger), DAC_V4_STAGGER
 
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
@@ -1293,12 +1283,6 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
     if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
-  if (g_conv3_stagger && a.stagger != g_conv3_stagger) {
-    ConvArgs b = a;
-    b.stagger = g_conv3_stagger;
-    conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(b, RW);
-    return true;
-  }
   conv3i_kernel<T, BM, BN, WGM, WGN, CK, ST, FL, EPK, WPE><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
   return true;
 }

@@ -49,8 +49,9 @@ template <typename T>
 static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
 // DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
 // Norm folding (LN into q|k|v / GEGLU / to_qkv, GroupNorm into proj_in's A path, GroupNorm
-// statistics from the PreNorm LayerNorm) on by default once validated on the GPU.
-constexpr bool kNormFoldDefault = false;
+// statistics from the PreNorm LayerNorm): on by default (validated: tests/test_normfold.py,
+// test_conv_kernels.py, the restoration-fixture bars).
+constexpr bool kNormFoldDefault = true;
 // DAC_NO_LN_FOLD=1 (read when a handle's weights are packed): SpatialTransformer norm1 / norm3
 // as separate LayerNorm launches (A/B aid; tests/test_lnfold.py).
 static bool no_ln_fold() {
@@ -482,8 +483,6 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
   a.lnf_cs = e.lnf_cs; a.lnf_n = e.lnf_n; a.lnf_eps = e.lnf_eps;
   a.gna_stats = e.gna_stats; a.gna_g = e.gna_g; a.gna_b = e.gna_b; a.gna_groups = e.gna_groups;
-  if (a.lnf_cs && !conv_lnf_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: LN fold requested on a shape without a folding kernel");
-  if (a.gna_stats && !conv_gna_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: GroupNorm A path requested on a shape without such a kernel");
   const double M = (double)B * a.Ho * a.Wo;
   double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   Profiler* p = r.prof;
@@ -509,6 +508,9 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     return;
   }
   if (!cw.w) throw Error(DAC_E_STATE, "conv weight not loaded");
+  // (Dry runs carry no zero page; the engine chose these paths with the same predicates.)
+  if (a.lnf_cs && !conv_lnf_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: LN fold requested on a shape without a folding kernel");
+  if (a.gna_stats && !conv_gna_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: GroupNorm A path requested on a shape without such a kernel");
   if (a.Cin % (16 / (int)sizeof(T)) || (a.x2 == nullptr && a.C1 < a.Cin))
     throw Error(DAC_E_ARG, "conv: bad channel layout");
   if (timed) {

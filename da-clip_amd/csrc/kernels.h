@@ -54,10 +54,6 @@ struct ConvArgs {
   const float* bias2;
   int w2_dual;
   void* y2; int ldy2;
-  // v4 3x3 tiles (tuning experiment, DAC_V4_STAGGER): first-round blocks of the upper half of
-  // the co-resident slots start `stagger` x 2048 clocks late, so two blocks sharing a CU run
-  // their epilogues out of phase. 0 = off.
-  int stagger;
   // Row LayerNorm of the INPUT folded into a 1x1 GEMM (SpatialTransformer norm1 -> q|k|v and
   // norm3 -> GEGLU proj, attention.py:253-261): the weights are pre-multiplied by the LN gain
   // (w = W diag(g)), bias = b + W beta, and the kernel takes the row moments of x from its own
