@@ -106,7 +106,9 @@ bool conv_lnf_ok(const ConvArgs& a, int elem_bytes) {
 // image, groups of whole 16-byte vectors (the groupnorm_stats layout), Cin <= 1024.
 bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.lnf_cs || a.y2 || a.up) return false;
-  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 1024 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64) return false;
+  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 1024 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64 ||
+      (a.gna_groups & (a.gna_groups - 1)))
+    return false;
   if (a.Cin % a.gna_groups || (a.Cin / a.gna_groups) % 8 || 256 % (a.Cin / 8)) return false;
   if (a.Cout % 128 || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8)) return false;
   return (a.act == ACT_NONE || a.act == ACT_SILU) && (a.Ho * a.Wo) % 64 == 0;

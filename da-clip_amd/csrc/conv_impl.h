@@ -374,7 +374,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
                           sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
-  constexpr int GTAB = GNA ? 8192 : 0;                  // (scale, shift) x Cin <= 1024 floats pairs
+  constexpr int GTAB = GNA ? 8192 + 512 : 0;            // (scale, shift) x Cin <= 1024, (mean, rstd) x 64
   constexpr int SMEM = (PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES) + GTAB;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -520,8 +520,26 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     // Channel c of this tile's image: s = rstd * gamma, t = beta - mean * s (tile in one image:
     // conv_gna_ok). Its loads overlap the first stage's DMA; read after the first barrier.
     const int bimg = m0 / HWo, cpg = a.Cin / a.gna_groups;
+    const float* stt = a.gna_stats + (size_t)bimg * a.gna_groups * 2;
+    if (a.gna_nb > 0) {
+      // Per-block (sum, sum of squares) of the PreNorm LayerNorm: tpg threads per group sum a
+      // strided share of the image's nb blocks, then a fixed xor tree (lanes of one wave).
+      float* gst = gtab + 2048;
+      const int tpg = 64 * NW / a.gna_groups, gi = tid / tpg, p = tid % tpg;
+      const float* pp = a.gna_stats + (size_t)(bimg * a.gna_groups + gi) * a.gna_nb * 2;
+      float s1 = 0.f, s2 = 0.f;
+      for (int k = p; k < a.gna_nb; k += tpg) { s1 += pp[2 * k]; s2 += pp[2 * k + 1]; }
+      for (int o = 1; o < tpg; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      if (p == 0) {
+        const float n = (float)HWo * (float)cpg, mu = s1 / n, var = fmaxf(s2 / n - mu * mu, 0.f);
+        gst[2 * gi] = mu;
+        gst[2 * gi + 1] = 1.f / sqrtf(var + a.gna_eps);
+      }
+      __syncthreads();
+      stt = gst;
+    }
     for (int c = tid; c < a.Cin; c += 64 * NW) {
-      const float* st = a.gna_stats + ((size_t)bimg * a.gna_groups + c / cpg) * 2;
+      const float* st = stt + (c / cpg) * 2;
       const float sc = st[1] * a.gna_g[c];
       gtab[2 * c] = sc;
       gtab[2 * c + 1] = a.gna_b[c] - st[0] * sc;

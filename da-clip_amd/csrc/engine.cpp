@@ -48,24 +48,19 @@ static int key_role(const std::string& k) {
 template <typename T>
 static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
 // DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
-// Norm folding (LN into q|k|v / GEGLU / to_qkv, GroupNorm into proj_in's A path, GroupNorm
-// statistics from the PreNorm LayerNorm): on by default (validated: tests/test_normfold.py,
-// test_conv_kernels.py, the restoration-fixture bars).
-constexpr bool kNormFoldDefault = true;
-// DAC_NO_LN_FOLD=1 (read when a handle's weights are packed): SpatialTransformer norm1 / norm3
-// as separate LayerNorm launches (A/B aid; tests/test_lnfold.py).
-static bool no_ln_fold() {
-  const char* e = getenv("DAC_NO_LN_FOLD");
-  if (e) return atoi(e) != 0;
-  return !kNormFoldDefault;
+// Norm folding switches (DAC_FOLD, a bit mask read when weights are packed and per forward):
+//   1 norm1 LayerNorm folded into the SpatialTransformer's q|k|v GEMM
+//   2 norm3 LayerNorm folded into the GEGLU proj
+//   4 the C = 256 LinearAttention PreNorm folded into to_qkv
+//   8 GroupNorm applied in proj_in's A path
+//  16 ... with its statistics taken by the PreNorm LayerNorm kernel (needs 8)
+// The default is the set measured faster in the network.
+constexpr int kFoldDefault = 1 | 4 | 8 | 16;
+static int fold_mask() {
+  const char* e = getenv("DAC_FOLD");
+  return e ? atoi(e) : kFoldDefault;
 }
-// DAC_NO_GN_IN_LN=1 (read per forward): GroupNorm statistics by their own pass (A/B aid).
-static bool no_gn_stats_in_ln() {
-  const char* e = getenv("DAC_NO_GN_IN_LN");
-  if (e) return atoi(e) != 0;
-  return !kNormFoldDefault;
-}
-static unsigned dry_count = 0;   // stands in for the device counters in dry runs (never touched)
+static bool fold_on(int bit) { return (fold_mask() & bit) != 0; }
 static bool no_res_fuse() {
   static const int v = getenv("DAC_NO_RES_FUSE") ? atoi(getenv("DAC_NO_RES_FUSE")) : 0;
   return v != 0;
@@ -483,6 +478,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.amode = e.amode; a.w_bstride = e.w_bstride; a.zero = r.zero; a.ln_g = e.ln_g; a.ln_eps = e.ln_eps;
   a.lnf_cs = e.lnf_cs; a.lnf_n = e.lnf_n; a.lnf_eps = e.lnf_eps;
   a.gna_stats = e.gna_stats; a.gna_g = e.gna_g; a.gna_b = e.gna_b; a.gna_groups = e.gna_groups;
+  a.gna_nb = e.gna_nb; a.gna_eps = e.gna_eps;
   const double M = (double)B * a.Ho * a.Wo;
   double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   Profiler* p = r.prof;
@@ -688,7 +684,7 @@ struct UNetNet {
       a.la.gpre = P.f32(p + "fn.norm.g", {1, C, 1, 1});
       std::vector<float> pq;
       a.la.qkv = P.conv(f + "to_qkv.weight", 384, C, 1, 1, "", false, 0, &pq);
-      if (sizeof(T) == 2 && !P.fp8 && !no_ln_fold() && C != 64 && C != 128) {
+      if (sizeof(T) == 2 && !P.fp8 && fold_on(4) && C != 64 && C != 128) {
         // The unfused LinearAttention path (C = 256): its channel LayerNorm (gain only) is
         // folded into to_qkv like the SpatialTransformer's norm1.
         auto fq = P.fold_ln(a.la.qkv, pq, 384, C, p + "fn.norm.g", "", nullptr, {1, C, 1, 1});
@@ -709,10 +705,13 @@ struct UNetNet {
     s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C, &pq);
     s.o = P.linear(b + "attn1.to_out.0.weight", C, C, b + "attn1.to_out.0.bias");
     s.ff1 = P.geglu(b + "ff.net.0.proj.weight", b + "ff.net.0.proj.bias", 4 * C, C, &pf, &pfb);
-    if (sizeof(T) == 2 && !P.fp8 && !no_ln_fold()) {
+    if (sizeof(T) == 2 && !P.fp8 && fold_on(1)) {
       auto fq = P.fold_ln(s.qkv, pq, 3 * C, C, b + "norm1.weight", b + "norm1.bias", nullptr);
+      if (fq.cs) { s.qkv_f = fq.cw; s.qkv_cs = fq.cs; }
+    }
+    if (sizeof(T) == 2 && !P.fp8 && fold_on(2)) {
       auto ff = P.fold_ln(s.ff1, pf, 8 * C, C, b + "norm3.weight", b + "norm3.bias", &pfb);
-      if (fq.cs && ff.cs) { s.qkv_f = fq.cw; s.qkv_cs = fq.cs; s.ff1_f = ff.cw; s.ff1_cs = ff.cs; }
+      if (ff.cs) { s.ff1_f = ff.cw; s.ff1_cs = ff.cs; }
     }
     s.ff2 = P.linear(b + "ff.net.2.weight", C, 4 * C, b + "ff.net.2.bias");
     // attn2 attends to ONE context token: softmax over a single key is exactly 1, so its
@@ -935,7 +934,7 @@ struct UNetNet {
   static bool gna_fits(int C, int Cout, int HW) {
     ConvArgs a{};
     a.zero = &a; a.Cin = a.C1 = a.K = C; a.Cout = a.ldy = Cout; a.gna_groups = 32; a.Ho = HW; a.Wo = 1;
-    return !no_ln_fold() && conv_gna_ok(a, (int)sizeof(T));
+    return fold_on(8) && conv_gna_ok(a, (int)sizeof(T));
   }
   static bool lnf_fits(int Cin, int Cout, int act, int HW) {
     ConvArgs a{};
@@ -953,22 +952,22 @@ struct UNetNet {
     // (mean, rstd) [B][32][2]; or the PreNorm LN's per-block group sums + the table.
     float* stats = r.alloc<float>(std::max((size_t)B * 32 * (32 * 3 + 2), layernorm_gnstats_ws_floats(B, L, 32)));
     T* hh = r.alloc<T>(M * C);
-    unsigned* cnt = B <= Run::kCounters ? r.counters : nullptr;
     if (gna_fits(C, C, L)) {
       // proj_in reads xn and applies the GroupNorm to its A fragments (no normalised copy); the
-      // GroupNorm statistics come out of the PreNorm LayerNorm's own pass when it can take them.
-      const float* tab = (cnt || r.dry) && !no_gn_stats_in_ln()
-                             ? layernorm_gnstats<T>(x, C, xn, C, s.gpre, nullptr, (int)M, C, 1e-5f, L, 32, 1e-6f,
-                                                    stats, r.dry ? &dry_count : cnt, !r.dry, r.st)
-                             : nullptr;
-      if (!tab) {
-        ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
-        tab = stats + (size_t)B * 32 * 32 * 3;
-        if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, cnt, r.st);
-      }
+      // GroupNorm statistics come out of the PreNorm LayerNorm's own pass when it can take them
+      // (per-block group sums, merged by proj_in's table fill).
       Epi ep;
-      ep.gna_stats = tab;
-      ep.gna_g = s.gnw; ep.gna_b = s.gnb; ep.gna_groups = 32;
+      const int nb = fold_on(16) ? layernorm_gnstats<T>(x, C, xn, C, s.gpre, nullptr, (int)M, C, 1e-5f, L, 32,
+                                                        stats, !r.dry, r.st)
+                                 : 0;
+      if (nb > 0) {
+        ep.gna_stats = stats; ep.gna_nb = nb;
+      } else {
+        ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
+        ep.gna_stats = stats + (size_t)B * 32 * 32 * 3;
+        if (!r.dry) groupnorm_stats<T>(xn, B, L, C, 32, 1e-6f, stats, r.st);
+      }
+      ep.gna_g = s.gnw; ep.gna_b = s.gnb; ep.gna_groups = 32; ep.gna_eps = 1e-6f;
       conv_call<T>(r, s.pin, xn, C, C, nullptr, 0, B, H, W, 0, 1, 0, hh, C, ep);
     } else {
       ln<T>(r, x, C, xn, C, nullptr, 0, s.gpre, nullptr, (int)M, C, 1e-5f);
@@ -1311,8 +1310,6 @@ class EngineT : public Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     zero_page = pool.alloc(256);
     HIP_OK(hipMemset(zero_page, 0, 256));
-    counters = (unsigned*)pool.alloc(Run::kCounters * sizeof(unsigned));
-    HIP_OK(hipMemset(counters, 0, Run::kCounters * sizeof(unsigned)));
     if (c.unet) unet = std::make_unique<UNetNet<T>>(c);
     if (c.vit) {
       if (c.image_size % c.patch_size || c.width % c.head_width || (c.head_width != 64 && c.head_width != 32) ||
@@ -1432,7 +1429,6 @@ class EngineT : public Engine {
     Run r;
     r.st = st;
     r.zero = zero_page;
-    r.counters = counters;
     r.dry = false;
     arena.dry = false;
     r.ar = &arena;
@@ -1646,7 +1642,6 @@ class EngineT : public Engine {
   hipEvent_t ev_in, ev_out;
   uint64_t noise_offset = 0;     // global index of image 0 (sharded runs)
   void* zero_page = nullptr;
-  unsigned* counters = nullptr;
 };
 
 std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {

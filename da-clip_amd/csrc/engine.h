@@ -106,9 +106,6 @@ struct Run {
   Arena* ar = nullptr;
   Profiler* prof = nullptr;
   const void* zero = nullptr;    // 256 zero bytes on the device (conv padding source)
-  // Zeroed device counters (kCounters); a kernel that counts in them puts them back to zero.
-  unsigned* counters = nullptr;
-  static constexpr int kCounters = 4096;
   double flops = 0;              // executed FLOPs (2*MAC) accumulated by the launches
   template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
 };
@@ -138,6 +135,8 @@ struct Epi {
   const float* gna_g = nullptr;
   const float* gna_b = nullptr;
   int gna_groups = 0;
+  int gna_nb = 0;                // > 0: gna_stats holds per-block group sums (ConvArgs::gna_nb)
+  float gna_eps = 1e-6f;
 };
 
 template <typename T>

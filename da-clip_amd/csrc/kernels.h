@@ -65,30 +65,33 @@ struct ConvArgs {
   // GroupNorm of the INPUT applied in a 1x1 GEMM's A path (SpatialTransformer norm ->
   // proj_in, attention.py:76-77, 239-241): the A fragments are mapped x -> x * s + t per
   // channel, s = rstd(b, g) * gamma, t = beta - mean(b, g) * s, rounded back to T (what a
-  // separate GroupNorm pass would have stored). gna_stats = [B][groups][mean, rstd].
+  // separate GroupNorm pass would have stored). gna_nb == 0: gna_stats = [B][groups][mean,
+  // rstd]; gna_nb > 0: gna_stats = [B][groups][gna_nb][sum, sum of squares] per-block sums of
+  // the PreNorm LayerNorm kernel (layernorm_gnstats), merged by every block in fixed order with
+  // eps gna_eps.
   const float* gna_stats;
   const float* gna_g;
   const float* gna_b;
   int gna_groups;
+  int gna_nb;
+  float gna_eps;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
 // ... and a kernel applying the input GroupNorm in its A path (ConvArgs::gna_stats).
 bool conv_gna_ok(const ConvArgs& a, int elem_bytes);
 // GroupNorm statistics only (norm.hip): the (mean, rstd) table groupnorm() applies, at
-// part + B * groups * GN_CHUNKS * 3 (returned). count: B zeroed device counters (left zeroed);
-// the last partial block of each image then merges it (one launch), else a gn_merge launch.
-// LayerNorm whose output also yields that tensor's GroupNorm statistics (norm.hip): returns the
-// (mean, rstd) table inside part, or nullptr if the shape is not covered; launch = false only
-// answers.
-template <typename T>
-const float* layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b,
-                               int rows, int C, float eps, int HW, int groups, float gn_eps, float* part,
-                               unsigned* count, bool launch, hipStream_t st);
-size_t layernorm_gnstats_ws_floats(int B, int HW, int groups);
+// part + B * groups * GN_CHUNKS * 3 (returned).
 template <typename T>
 const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part,
-                             unsigned* count, hipStream_t st);
+                             hipStream_t st);
+// LayerNorm whose output also yields that tensor's GroupNorm statistics (norm.hip): per-block
+// group sums [B][groups][nb][sum, sum of squares] into part; returns nb (blocks per image), or 0
+// if the shape is not covered; launch = false only answers.
+template <typename T>
+int layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b, int rows, int C,
+                      float eps, int HW, int groups, float* part, bool launch, hipStream_t st);
+size_t layernorm_gnstats_ws_floats(int B, int HW, int groups);
 // The dispatcher can fuse a_w2/y2 into this 3x3 conv (bf16 v4 256x64 swapped-operand tiles).
 bool conv_res_fusable(const ConvArgs& a);
 

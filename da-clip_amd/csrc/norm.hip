@@ -13,9 +13,10 @@ namespace dac {
 // GroupNorm statistics of the LayerNorm OUTPUT, taken by the LayerNorm kernel itself (GNS):
 // the SpatialTransformer's PreNorm LN feeds its GroupNorm (attention.py:239-241), so the
 // GroupNorm's pass over the data is the LN's own. Per block (one image's RPB rows) plain sums
-// (sum y, sum y^2) per group, written in fixed order; the image's last block merges its
-// blocks' sums into (mean, rstd) (count[b]: zeroed counters, left zeroed).
-struct GnStats { float* part; unsigned* count; int HW, groups; float eps; };
+// (sum y, sum y^2) per group, written in fixed order; the consumer (proj_in's GroupNorm-in-A
+// table, conv_impl.h EPI_GNA) merges an image's blocks in fixed order. No atomics or fences:
+// the kernel boundary publishes the sums.
+struct GnStats { float* part; int HW, groups; };
 
 // G lanes per row (power of two), NVL 16-byte vectors per lane.
 template <typename T, int G, int NVL, bool GNS = false>
@@ -112,56 +113,36 @@ __global__ void __launch_bounds__(256) ln_kernel(const T* __restrict__ x, int ld
       float* o = gs.part + (((size_t)img * gs.groups + t) * nb + blk) * 2;
       o[0] = a0; o[1] = a1;
     }
-    __shared__ unsigned last;
-    __threadfence();                             // block sums visible device-wide (all XCDs)
-    __syncthreads();
-    if (t == 0) last = atomicAdd(gs.count + img, 1u) == (unsigned)nb - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();                             // acquire the other blocks' sums
-    if (t < gs.groups) {
-      const float* pp = gs.part + ((size_t)img * gs.groups + t) * nb * 2;
-      float a0 = 0.f, a1 = 0.f;
-      for (int k = 0; k < nb; ++k) { a0 += __builtin_nontemporal_load(pp + 2 * k); a1 += __builtin_nontemporal_load(pp + 2 * k + 1); }
-      const float n = (float)gs.HW * (float)(C / gs.groups);
-      const float mu = a0 / n, var = fmaxf(a1 / n - mu * mu, 0.f);
-      float* o = gs.part + (size_t)(rows / gs.HW) * gs.groups * nb * 2 + ((size_t)img * gs.groups + t) * 2;
-      o[0] = mu;
-      o[1] = 1.f / sqrtf(var + gs.eps);
-    }
-    if (t == 0) atomicExch(gs.count + img, 0u);
   }
 }
 
-// LayerNorm (gain, bias) whose output also yields the GroupNorm(groups) statistics; 16-bit rows
-// of 256 or 512 channels (the SpatialTransformer widths), HW a multiple of the block's rows.
-// Returns the (mean, rstd) table, at part + (rows / HW) * groups * nb * 2, or nullptr when the
-// shape is not covered (the caller then runs layernorm + groupnorm_stats). launch = false only
-// answers (the engine's dry run).
+// LayerNorm (gain, bias) whose output also yields the GroupNorm(groups) per-block sums; 16-bit
+// rows of 256 or 512 channels (the SpatialTransformer widths), HW a multiple of the block's
+// rows. Returns the blocks per image (the sums are part[B][groups][nb][2]), or 0 when the shape
+// is not covered (the caller then runs layernorm + groupnorm_stats). launch = false only answers.
 template <typename T>
-const float* layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b,
-                               int rows, int C, float eps, int HW, int groups, float gn_eps, float* part,
-                               unsigned* count, bool launch, hipStream_t st) {
+int layernorm_gnstats(const void* x, int ldx, void* y, int ldy, const float* g, const float* b, int rows, int C,
+                      float eps, int HW, int groups, float* part, bool launch, hipStream_t st) {
   constexpr int VE = TypeInfo<T>::VE;
   const int NV = C / VE;
 #define LNG(G, NVL)                                                                                 \
   {                                                                                                 \
     constexpr int RPB = 4 * (64 / G);                                                               \
     const int vpg = groups > 0 && C % groups == 0 ? C / groups / VE : 0;                            \
-    if (vpg < 1 || G % vpg || (C / groups) % VE || HW % RPB || rows % HW || groups > 64 || !count)  \
-      return nullptr;                                                                               \
+    if (vpg < 1 || G % vpg || (C / groups) % VE || HW % RPB || rows % HW || groups > 64)            \
+      return 0;                                                                                     \
     if (launch)                                                                                     \
       ln_kernel<T, G, NVL, true><<<rows / RPB, 256, 0, st>>>((const T*)x, ldx, (T*)y, ldy, nullptr, \
                                                              0, g, b, rows, C, eps,                 \
-                                                             GnStats{part, count, HW, groups, gn_eps}); \
-    return part + (size_t)(rows / HW) * groups * (HW / RPB) * 2;                                    \
+                                                             GnStats{part, HW, groups});            \
+    return HW / RPB;                                                                                \
   }
   if (sizeof(T) == 2 && NV == 32) LNG(8, 4)
   if (sizeof(T) == 2 && NV == 64) LNG(16, 4)
 #undef LNG
-  return nullptr;
+  return 0;
 }
-// Workspace floats of layernorm_gnstats (block sums + the table), an upper bound.
+// Workspace floats of layernorm_gnstats (block sums), an upper bound.
 size_t layernorm_gnstats_ws_floats(int B, int HW, int groups) { return (size_t)B * groups * (2 * (HW / 16) + 2); }
 
 template <typename T>
@@ -220,8 +201,7 @@ DEV Moments chan_merge(Moments a, Moments b) {
 
 template <typename T>
 __global__ void __launch_bounds__(256) gn_partial(const T* __restrict__ x, float* part, int HW,
-                                                  int C, int groups, unsigned* count = nullptr,
-                                                  float eps = 0.f) {
+                                                  int C, int groups) {
   constexpr int VE = TypeInfo<T>::VE;
   const int b = blockIdx.y, ch = blockIdx.x;
   const int NV = C / VE;                         // vectors per pixel (<= 256)
@@ -259,28 +239,6 @@ __global__ void __launch_bounds__(256) gn_partial(const T* __restrict__ x, float
     float* o = part + (((size_t)b * groups + g) * GN_CHUNKS + ch) * 3;
     o[0] = r.n; o[1] = r.mean; o[2] = r.m2;
   }
-  if (!count) return;
-  // Merge in the image's last chunk block (count[b] = chunk blocks done; the merging block puts
-  // it back to 0 for the next launch). Fixed merge order: identical to gn_merge's result.
-  __shared__ unsigned last;
-  __threadfence();                               // partials visible device-wide (all XCDs)
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(count + b, 1u) == GN_CHUNKS - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();                               // acquire the other blocks' partials
-  if ((int)threadIdx.x < groups) {
-    const int g = threadIdx.x;
-    const float* pp = part + ((size_t)b * groups + g) * GN_CHUNKS * 3;
-    Moments r{0.f, 0.f, 0.f};
-    for (int k = 0; k < GN_CHUNKS; ++k)
-      r = chan_merge(r, Moments{__builtin_nontemporal_load(pp + 3 * k), __builtin_nontemporal_load(pp + 3 * k + 1),
-                                __builtin_nontemporal_load(pp + 3 * k + 2)});
-    float* o = part + (size_t)gridDim.y * groups * GN_CHUNKS * 3 + ((size_t)b * groups + g) * 2;
-    o[0] = r.mean;
-    o[1] = 1.f / sqrtf(r.m2 / r.n + eps);
-  }
-  if (threadIdx.x == 0) atomicExch(count + b, 0u);
 }
 
 // Pass 2 (gn_merge): one thread per (image, group) merges its GN_CHUNKS partials in fixed
@@ -395,23 +353,19 @@ void groupnorm(const void* x, void* y, const float* g, const float* b, int B, in
 
 template <typename T>
 const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, float eps, float* part,
-                             unsigned* count, hipStream_t st) {
+                             hipStream_t st) {
   constexpr int VE = TypeInfo<T>::VE;
   const int NV = C / VE;
   if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64) abort();   // conv_gna_ok checks this
-  if (count) {
-    gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups, count, eps);
-  } else {
-    gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
-    gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
-  }
+  gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
+  gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
   return part + (size_t)B * groups * GN_CHUNKS * 3;
 }
 
 #define INST(T)                                                                              \
-  template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, unsigned*, hipStream_t); \
-  template const float* layernorm_gnstats<T>(const void*, int, void*, int, const float*, const float*, int, int, \
-                                             float, int, int, float, float*, unsigned*, bool, hipStream_t); \
+  template const float* groupnorm_stats<T>(const void*, int, int, int, int, float, float*, hipStream_t); \
+  template int layernorm_gnstats<T>(const void*, int, void*, int, const float*, const float*, int, int, float, \
+                                    int, int, float*, bool, hipStream_t);                            \
   template void layernorm<T>(const void*, int, void*, int, const void*, int, const float*,  \
                              const float*, int, int, float, hipStream_t);                   \
   template void groupnorm<T>(const void*, void*, const float*, const float*, int, int, int, \
