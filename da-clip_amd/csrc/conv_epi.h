@@ -95,7 +95,10 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int lr = lane & 15, lg = lane >> 4;
-  const bool geglu = (EPK & EPI_GEGLU) && a.act == ACT_GEGLU;
+  // EPK == EPI_GEGLU kernels are launched for GEGLU only: compile only that path (the runtime
+  // choice kept the other one live and pushed the accumulators to scratch).
+  constexpr bool GEGLU_ONLY = EPK == EPI_GEGLU;
+  const bool geglu = GEGLU_ONLY || ((EPK & EPI_GEGLU) && a.act == ACT_GEGLU);
   const bool fast = !(EPK & EPI_GENERAL) || bimg >= 0;
   float* tile = reinterpret_cast<float*>(smem);
 
@@ -209,10 +212,10 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int j = 0; j < TN; j += 2)
-            acc[i][j][r] = (acc[i][j][r] + bi[j]) * gelu_fast(acc[i][j + 1][r] + bi[j + 1]);
+          for (int j2 = 0; j2 < TN / 2; ++j2)
+            acc[i][2 * j2][r] = (acc[i][2 * j2][r] + bi[2 * j2]) * gelu_fast(acc[i][2 * j2 + 1][r] + bi[2 * j2 + 1]);
     }
-  } else if (fast) {
+  } else if (!GEGLU_ONLY && fast) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -276,9 +279,9 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
           if (geglu) {
             if constexpr (TN % 2 == 0) {
 #pragma unroll
-              for (int j = 0; j < TN; j += 2) row[(wn * WTN + j * 16) / 2 + lr] = acc[i][j][r];
+              for (int j2 = 0; j2 < TN / 2; ++j2) row[(wn * WTN + j2 * 32) / 2 + lr] = acc[i][2 * j2][r];
             }
-          } else {
+          } else if constexpr (!GEGLU_ONLY) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) row[wn * WTN + j * 16 + lr] = acc[i][j][r];
           }
