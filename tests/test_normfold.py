@@ -1,10 +1,10 @@
 """The SpatialTransformer / LinearAttention norm folds in the network (engine.cpp sptrans /
-linattn): norm1 and norm3 LayerNorms folded into q|k|v and the GEGLU proj, the GroupNorm applied
-in proj_in's A path with its statistics from the PreNorm LayerNorm, and the C = 256
-LinearAttention PreNorm folded into to_qkv (attention.py:76-77, 239-261; module_util.py:77-97,
-157-185). One bf16 256x256 forward (every folded shape at the 32x32 / 64x64 levels) with the folds
-on and off (DAC_NO_LN_FOLD / DAC_NO_GN_IN_LN, read when the handle packs its weights and per
-forward), each against the fp32 numpy oracle: the folded path must be as close to the oracle as
+linattn): the norm1 LayerNorm folded into q|k|v, the GroupNorm applied in proj_in's A path with
+its statistics from the PreNorm LayerNorm, and the C = 256 LinearAttention PreNorm folded into
+to_qkv (attention.py:76-77, 239-261; module_util.py:77-97, 157-185). One bf16 256x256 forward
+(every folded shape at the 32x32 / 64x64 levels) with the folds on (the default DAC_FOLD mask)
+and off (DAC_FOLD=0, read when the handle packs its weights and per forward), each against the
+fp32 numpy oracle: the folded path must be as close to the oracle as
 the unfolded one (bound 1.5e-2 max-rel, the bf16 forward bar of test_hip_parity.py), and the two
 bf16 outputs must agree to bf16 noise."""
 import os
@@ -24,9 +24,11 @@ def rel(a, b):
 
 def _forward(unet_sd, fold, x, mu, tc, ic):
     from daclip_amd.unet import ConditionalUNet
-    old = {k: os.environ.get(k) for k in ("DAC_NO_LN_FOLD", "DAC_NO_GN_IN_LN")}
-    os.environ["DAC_NO_LN_FOLD"] = "0" if fold else "1"
-    os.environ["DAC_NO_GN_IN_LN"] = "0" if fold else "1"
+    old = {k: os.environ.get(k) for k in ("DAC_FOLD",)}
+    if fold:
+        os.environ.pop("DAC_FOLD", None)
+    else:
+        os.environ["DAC_FOLD"] = "0"
     try:
         m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype="bf16")
         m.load_state_dict(unet_sd)
