@@ -87,13 +87,16 @@ def parse():
     p.add_argument("--modes", default="fp16",
                    help="comma-separated extra dtypes measured after the main line on 1 GPU (throughput "
                         "+ PSNR vs the reference), reported under 'modes'; 'none' to skip")
-    p.add_argument("--kernel-id", type=int, default=312,
-                   help="conv class timed for the roofline (kh*100 + variant; 312 = 3x3 interleaved-row v4 tiles)")
+    p.add_argument("--kernel-id", type=int, default=None,
+                   help="conv class timed for the roofline (kh*100 + variant; default 312 = 3x3 "
+                        "interleaved-row v4 tiles, 330 = the fp8 3x3 kernel for --dtype fp8)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the bf16-vs-fp32 PSNR sample")
     p.add_argument("--cpu-steps", type=int, default=5, help="UNet steps in the CPU sample (>= 5)")
     a = p.parse_args()
+    if a.kernel_id is None:
+        a.kernel_id = 330 if a.dtype == "fp8" else 312
     wild = a.model == "wild-ir"
     a.batch = a.batch or (2 if wild else 8)
     a.res = a.res or (512 if wild else 256)
