@@ -1,4 +1,4 @@
-# Norm folds: op checks, A/B bench runs per fold bit set, rocprof kernel stats of the default.
+# Norm folds A/B: op checks, bench runs per DAC_FOLD mask, rocprof kernel stats of the default.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -1,4 +1,4 @@
-# Which fold breaks fp16 batch invariance on the restoration fixture.
+# Which DAC_FOLD mask breaks fp16 batch invariance on the restoration fixture (bit 2 = the GEGLU fold, since removed from the engine).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for m in 0 29 2 31 1 8 24; do
