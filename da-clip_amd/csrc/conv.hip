@@ -103,10 +103,10 @@ bool conv_lnf_ok(const ConvArgs& a, int elem_bytes) {
 }
 
 // Mirrors the EPI_GNA branch of conv_dispatch: 1x1, 16-bit, 64x128 swapped tiles inside one
-// image, groups of whole 16-byte vectors (the groupnorm_stats layout), Cin <= 1024.
+// image, groups of whole 16-byte vectors (the groupnorm_stats layout), Cin <= 512.
 bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.lnf_cs || a.y2 || a.up) return false;
-  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 1024 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64 ||
+  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 512 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64 ||
       (a.gna_groups & (a.gna_groups - 1)))
     return false;
   if (a.Cin % a.gna_groups || (a.Cin / a.gna_groups) % 8 || 256 % (a.Cin / 8)) return false;

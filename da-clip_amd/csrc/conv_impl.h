@@ -374,7 +374,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
                           sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
-  constexpr int GTAB = GNA ? 8192 + 512 : 0;            // (scale, shift) x Cin <= 1024, (mean, rstd) x 64
+  // (scale, shift) x Cin <= 512, (mean, rstd) x 64 groups: 4.5 KB, so three 64x128 blocks still
+  // share a CU (3 x 53.75 KB).
+  constexpr int GTAB = GNA ? 4096 + 512 : 0;
   constexpr int SMEM = (PIPE > EpiLds<EPR, BN>::BYTES ? PIPE : EpiLds<EPR, BN>::BYTES) + GTAB;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
@@ -524,7 +526,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     if (a.gna_nb > 0) {
       // Per-block (sum, sum of squares) of the PreNorm LayerNorm: tpg threads per group sum a
       // strided share of the image's nb blocks, then a fixed xor tree (lanes of one wave).
-      float* gst = gtab + 2048;
+      float* gst = gtab + 1024;
       const int tpg = 64 * NW / a.gna_groups, gi = tid / tpg, p = tid % tpg;
       const float* pp = a.gna_stats + (size_t)(bimg * a.gna_groups + gi) * a.gna_nb * 2;
       float s1 = 0.f, s2 = 0.f;
