@@ -20,40 +20,52 @@ __device__ __forceinline__ float act_f(float v, int a) {
   return a == ACT_SILU ? silu_f(v) : a == ACT_GELU ? gelu_f(v) : v;
 }
 
-// One wave per output element group; lanes split the reduction (coalesced W rows).
+// Block = SL_R rows x 32 outputs, one thread per (row, output): the block's input rows are
+// staged in LDS once (with the pre-activation) and every W row is read by the SL_R threads of
+// its output from L1/L2 (16-byte loads), instead of once per (row, 32 outputs) block; each
+// output is one thread's fixed-order sum, so results do not depend on R (batch invariance).
+constexpr int SL_R = 8;
 __global__ void __launch_bounds__(256) small_linear_kernel(const float* __restrict__ x, int ldx,
                                                            const float* __restrict__ W,
                                                            const float* b, float* y, int ldy,
                                                            int R, int I, int O, int pre,
                                                            int post, const float* add,
                                                            int add_ld, int add_mod) {
-  extern __shared__ float xs[];
-  const int r = blockIdx.y;
-  for (int i = threadIdx.x; i < I; i += 256) xs[i] = act_f(x[(size_t)r * ldx + i], pre);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o0 = blockIdx.x * 32 + wave * 8;
-  for (int oi = 0; oi < 8; ++oi) {
-    const int o = o0 + oi;
-    if (o >= O) break;
-    float s = 0.f;
-    for (int i = lane; i < I; i += 64) s += xs[i] * W[(size_t)o * I + i];
-    s = wave_sum(s);
-    if (lane == 0) {
-      float v = s + (b ? b[o] : 0.f);
-      v = act_f(v, post);
-      if (add) v += add[(size_t)(r % add_mod) * add_ld + o];
-      y[(size_t)r * ldy + o] = v;
-    }
+  extern __shared__ float xs[];                 // [SL_R][I]
+  const int r0 = blockIdx.y * SL_R;
+  for (int k = threadIdx.x; k < SL_R * I; k += 256) {
+    const int rr = k / I, i = k - rr * I;
+    xs[k] = r0 + rr < R ? act_f(x[(size_t)(r0 + rr) * ldx + i], pre) : 0.f;
   }
+  __syncthreads();
+  const int rr = threadIdx.x >> 5, o = blockIdx.x * 32 + (threadIdx.x & 31), r = r0 + rr;
+  if (o >= O || r >= R) return;
+  const float* wr = W + (size_t)o * I;
+  const float* xr = xs + rr * I;
+  float s = 0.f;
+  if ((I & 3) == 0 && ((uintptr_t)W & 15) == 0) {
+    for (int i = 0; i < I; i += 4) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wr + i);
+      s = fmaf(xr[i], w[0], s);
+      s = fmaf(xr[i + 1], w[1], s);
+      s = fmaf(xr[i + 2], w[2], s);
+      s = fmaf(xr[i + 3], w[3], s);
+    }
+  } else {
+    for (int i = 0; i < I; ++i) s = fmaf(xr[i], wr[i], s);
+  }
+  float v = s + (b ? b[o] : 0.f);
+  v = act_f(v, post);
+  if (add) v += add[(size_t)(r % add_mod) * add_ld + o];
+  y[(size_t)r * ldy + o] = v;
 }
 
 void small_linear(const float* x, int ldx, const float* W, const float* b, float* y, int ldy,
                   int R, int I, int O, int pre, int post, const float* add, int add_ld,
                   int add_mod, hipStream_t st) {
-  dim3 g((O + 31) / 32, R);
-  small_linear_kernel<<<g, 256, I * sizeof(float), st>>>(x, ldx, W, b, y, ldy, R, I, O, pre,
-                                                          post, add, add_ld, add_mod > 0 ? add_mod : 1);
+  dim3 g((O + 31) / 32, (R + SL_R - 1) / SL_R);
+  small_linear_kernel<<<g, 256, SL_R * I * sizeof(float), st>>>(x, ldx, W, b, y, ldy, R, I, O, pre,
+                                                                 post, add, add_ld, add_mod > 0 ? add_mod : 1);
 }
 
 __global__ void __launch_bounds__(256) softmax_mul_kernel(const float* x, const float* v,
