@@ -44,13 +44,16 @@ __global__ void __launch_bounds__(256) small_linear_kernel(const float* __restri
   const float* xr = xs + rr * I;
   float s = 0.f;
   if ((I & 3) == 0 && ((uintptr_t)W & 15) == 0) {
+    // Four independent partial sums (combined in a fixed order): the FMA chain is not one
+    // I-long dependency.
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
     for (int i = 0; i < I; i += 4) {
       const f32x4 w = *reinterpret_cast<const f32x4*>(wr + i);
-      s = fmaf(xr[i], w[0], s);
-      s = fmaf(xr[i + 1], w[1], s);
-      s = fmaf(xr[i + 2], w[2], s);
-      s = fmaf(xr[i + 3], w[3], s);
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(xr + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s4[e] = fmaf(xv[e], w[e], s4[e]);
     }
+    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   } else {
     for (int i = 0; i < I; ++i) s = fmaf(xr[i], wr[i], s);
   }
