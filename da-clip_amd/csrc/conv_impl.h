@@ -1337,6 +1337,12 @@ bool conv3i_launch(int cfg, const ConvArgs& a, hipStream_t st) {
     case 49:
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 1024>(a, st);
       return false;
+    case 52:   // 48 with s_setprio(1) around each stage's MFMAs (FL bit 2)
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 4>(a, st);
+      return false;
+    case 53:   // 48 with sched_barrier fences around each stage (FL bit 0)
+      if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 1>(a, st);
+      return false;
     case 50:   // diagnostic: 48 with every A row read from a 256-pixel (L2-resident) window
       if constexpr (sizeof(T) == 2) return a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 2048>(a, st);
       return false;
