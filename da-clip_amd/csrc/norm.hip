@@ -15,7 +15,9 @@ namespace dac {
 // GroupNorm's pass over the data is the LN's own. Per block (one image's RPB rows) plain sums
 // (sum y, sum y^2) per group, written in fixed order; the consumer (proj_in's GroupNorm-in-A
 // table, conv_impl.h EPI_GNA) merges an image's blocks in fixed order. No atomics or fences:
-// the kernel boundary publishes the sums.
+// the kernel boundary publishes the sums. The sums are of the fp32 LayerNorm outputs, before
+// their rounding to T (the separate GroupNorm pass read the rounded copy: a difference of the
+// order of the storage rounding, averaged over a group).
 struct GnStats { float* part; int HW, groups; };
 
 // G lanes per row (power of two), NVL 16-byte vectors per lane.
