@@ -90,15 +90,13 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
 // no forced configuration, the swapped tiles' 16-byte scale / shift / bias DMA); the dispatcher
 // aborts if neither launches, so y2 is never left unwritten.
 // Mirrors the EPI_LNF branch of conv_dispatch (conv_impl.h): 1x1, 16-bit, whole 16-byte rows,
-// tiles inside one image; GEGLU on 256x256 tiles, the rest on 64x128 swapped tiles.
+// tiles inside one image, 64x128 swapped tiles; no GEGLU (the tile that folded it is gone).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.y2 || a.up) return false;
   if (a.Cin % 64 || a.Cout % 8 || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8)) return false;
   if (a.x2 && a.C1 < a.Cin) return false;
   const int HWo = a.Ho * a.Wo;
   const bool batched = a.w_bstride > 0;
-  if (a.act == ACT_GEGLU)
-    return !a.res1 && !a.res2 && !a.bbias && !a.ss && (batched || HWo % 256 == 0) && a.Cout % 256 == 0;
   return (a.act == ACT_NONE || a.act == ACT_SILU) && (batched || HWo % 64 == 0) && a.Cout % 128 == 0;
 }
 
@@ -106,7 +104,9 @@ bool conv_lnf_ok(const ConvArgs& a, int elem_bytes) {
 // image, groups of whole 16-byte vectors (the groupnorm_stats layout), Cin <= 512.
 bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.ln_g || a.lnf_cs || a.y2 || a.up) return false;
-  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 512 || a.Cin != a.K || a.gna_groups <= 0 || a.gna_groups > 64 ||
+  // gna_groups >= 4: the statistics merge reduces tpg = 256 / groups lanes with an xor tree
+  // inside one wave (conv_impl.h), so a group may not span two waves.
+  if (a.x2 || a.w_bstride || a.Cin % 64 || a.Cin > 512 || a.Cin != a.K || a.gna_groups < 4 || a.gna_groups > 64 ||
       (a.gna_groups & (a.gna_groups - 1)))
     return false;
   if (a.Cin % a.gna_groups || (a.Cin / a.gna_groups) % 8 || 256 % (a.Cin / 8)) return false;

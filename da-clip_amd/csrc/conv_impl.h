@@ -1771,13 +1771,10 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
     }
     if constexpr (KH == 1) if (a.lnf_cs) {
       // Input LayerNorm folded in (conv_lnf_ok mirrors these two choices).
+      // (Swapped 64x128 tiles only. A 256x256 GEGLU | LNF tile existed in round 3; its fp16
+      // outputs depended on the batch composition and it was slower than the unfolded chain, so
+      // it was removed together with conv_lnf_ok's GEGLU case.)
       if constexpr (sizeof(T) == 2) {
-        if (a.act == ACT_GEGLU && rows_ok && !a.res1 && !a.res2 && !a.bbias && !a.ss && (batched || HWo % 256 == 0) &&
-            a.Cout % 256 == 0) {
-          dim3 g((Mg + 255) / 256, a.Cout / 256, gz);
-          conv2_kernel<T, 256, 256, 4, 2, 2, KH, KW, S, P, EPI_GEGLU | EPI_LNF><<<g, 512, 0, st>>>(a);
-          return;
-        }
         if (a.act != ACT_GEGLU && minimal(64) && a.Cout % 128 == 0) {
           dim3 g((Mg + 63) / 64, a.Cout / 128, gz);
           conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_LNF><<<g, 256, 0, st>>>(a);

@@ -50,8 +50,8 @@ static void emu_round(const Run& r, void* y, int ld, size_t rows, int C);
 // DAC_NO_RES_FUSE=1: run each ResBlock res_conv as its own launch (A/B switch).
 // Norm folding switches (DAC_FOLD, a bit mask read when weights are packed and per forward):
 //   1 norm1 LayerNorm folded into the SpatialTransformer's q|k|v GEMM
-//   2 (reserved: norm3 folded into the GEGLU proj measured slower and, in fp16 handles, not
-//      batch-invariant on the restoration fixture; not built)
+//   2 (unused: norm3 folded into the GEGLU proj measured slower and, in fp16 handles, not
+//      batch-invariant on the restoration fixture; its kernel was deleted in round 4)
 //   4 the C = 256 LinearAttention PreNorm folded into to_qkv
 //   8 GroupNorm applied in proj_in's A path
 //  16 ... with its statistics taken by the PreNorm LayerNorm kernel (needs 8)

@@ -178,8 +178,11 @@ def create_model(model_name: str, pretrained: Optional[str] = None, precision: s
     if model_name not in arch.MODEL_CONFIGS:
         raise RuntimeError(f"Model config for {model_name} not found.")
     v, t = arch.MODEL_CONFIGS[model_name]
-    dt = dtype or ("bf16" if precision in ("bf16", "pure_bf16", "amp_bf16") else
-                   "fp16" if precision in ("fp16", "pure_fp16", "amp") else "fp32")
+    # factory.py:198-219: 'fp16'/'bf16' (manual mixed precision) and 'pure_fp16'/'pure_bf16'
+    # store the weights in 16 bits; 'amp' / 'amp_bf16' keep fp32 weights (autocast is the
+    # caller's business there), so they map to the fp32 handles here too.
+    dt = dtype or ("bf16" if precision in ("bf16", "pure_bf16") else
+                   "fp16" if precision in ("fp16", "pure_fp16") else "fp32")
     model = DaCLIP(v, t, device=device, dtype=dt)
     if pretrained:
         if not os.path.exists(pretrained):

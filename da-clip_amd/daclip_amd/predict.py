@@ -71,6 +71,9 @@ class Predictor:
         self.model.feed_data(noisy, lq, text_context=dc, image_context=ic)
         self.model.test(self.sde, mode=self.mode, noises=noises)
         out = self.model.get_current_visuals(need_GT=False)["Outputs"]
+        if not torch.isfinite(out).all():
+            # 16-bit storage (fp16 saturates at 65504) must never turn into silent garbage pixels.
+            raise RuntimeError(f"Predictor: non-finite restored output ({self.model.model.dtype} handles)")
         return [tensor2img(o) for o in out]
 
     def predict(self, image: Union[str, np.ndarray], noise: Optional[torch.Tensor] = None,
