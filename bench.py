@@ -88,6 +88,12 @@ def parse():
     p.add_argument("--modes", default="bf16",
                    help="comma-separated extra dtypes measured after the main line on 1 GPU (throughput "
                         "+ PSNR vs the reference), reported under 'modes'; 'none' to skip")
+    p.add_argument("--lines", default="wild-ir,fp8,fp32",
+                   help="comma-separated extra configuration lines measured after the main line on 1 GPU "
+                        "(one warmup + min(steps, 2) timed restores each), reported under 'lines': wild-ir = "
+                        "BASELINE configs[3]'s per-GPU slice (ViT-L/14 + scale-0.5 UNet, 512^2, 2 images), fp8 = "
+                        "configs[4]'s per-GPU slice (256^2, 16 images, e4m3 GEMMs), fp32 = the parity mode on the "
+                        "main workload; 'none' to skip")
     p.add_argument("--kernel-id", type=int, default=None,
                    help="conv class timed for the roofline (kh*100 + variant; default 312 = 3x3 "
                         "interleaved-row v4 tiles, 330 = the fp8 3x3 kernel for --dtype fp8)")
@@ -337,6 +343,48 @@ def timed_steps(step, warmup, steps, ws, dev):
     return out, el
 
 
+LINES = {
+    # name: (model, resolution, images per GPU, dtype or None = the main line's, BASELINE config)
+    "wild-ir": ("wild-ir", 512, 2, None, "configs[3] per-GPU slice: Wild-IR 512x512, 16 images over 8 GPUs"),
+    "fp8": ("universal-ir", 256, 16, "fp8", "configs[4] per-GPU slice: fp8 GEMMs, 256x256, 128 images over 8 GPUs"),
+    "fp32": ("universal-ir", 256, 8, "fp32", "configs[1] workload in the fp32 parity mode"),
+}
+
+
+def extra_line(args, name, dev):
+    """One more BASELINE configuration on this GPU (driver-observed in the same run): its own
+    handles with the seeded synthetic weights, the same step as the main line (encode ->
+    noise_state -> T-step graph loop), one warmup and min(steps, 2) timed restores."""
+    from daclip_amd import arch, synth
+    from daclip_amd.unet import ConditionalUNet
+    from daclip_amd.open_clip import DaCLIP
+    from daclip_amd.sde import IRSDE
+    model, R, B, dt, what = LINES[name]
+    a2 = argparse.Namespace(**vars(args))
+    a2.model, a2.res, a2.batch, a2.dtype = model, R, B, dt or args.dtype
+    t0 = time.perf_counter()
+    ucfg, ukw, vcfg, tcfg = model_setup(a2)
+    uspec = arch.unet_state_spec(ucfg)
+    cspec = {k: s for k, s in arch.daclip_state_spec(vcfg, tcfg).items() if k.startswith(("clip.visual.", "visual_control."))}
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], **ukw, device=dev, dtype=a2.dtype)
+    unet.load_state_dict(synth.synth_state_dict(uspec, 0))
+    clip = DaCLIP(vcfg, tcfg, device=dev, dtype=a2.dtype, with_text=False)
+    clip.load_state_dict(synth.synth_state_dict(cspec, 0), strict=False)
+    sde = IRSDE(max_sigma=50, T=a2.T, schedule="cosine", eps=0.005)
+    sde.set_model(unet)
+    n, lo, lq, img = shard_inputs(B, R, 1, 0, dev)
+    out, el = timed_steps(make_step(clip, sde, lq, img, lo, n, 1), 1, min(args.steps, 2), 1, dev)
+    k = min(args.steps, 2)
+    res = {"line": name, "config": what, "model": model, "dtype": a2.dtype, "resolution": R, "batch_per_gpu": B,
+           "value": round(B * k / el, 4), "unit": "images/s", "ms_per_step": round(el / k * 1e3, 2), "steps": k,
+           "outputs_finite": bool(torch.isfinite(out).all().item()),
+           "model_tflop_per_image": round((a2.T * unet.flops(B, R, R) + clip.flops(B)) / B / 1e12, 3)}
+    if model == "universal-ir" and a2.T == 100 and not args.no_psnr:
+        res["psnr"] = psnr_vs_reference(a2, clip, dev)
+    res["wall_s"] = round(time.perf_counter() - t0, 1)
+    return res
+
+
 def main():
     args = parse()
     ws, rank, local = setup_dist(args)
@@ -446,6 +494,15 @@ def main():
         modes = [m for m in args.modes.split(",") if m and m != "none" and m != args.dtype]
         if ws == 1 and modes:
             res["modes"] = [extra_mode(args, m, dev, lq, img4clip, uspec, cspec) for m in modes]
+        lines = [x for x in args.lines.split(",") if x and x != "none"]
+        if ws == 1 and args.model == "universal-ir" and lines:
+            res["lines"] = []
+            for x in lines:
+                if x not in LINES:
+                    raise SystemExit(f"bench: unknown line {x!r} (choose from {sorted(LINES)})")
+                if LINES[x][3] == args.dtype and LINES[x][1] == args.res and LINES[x][2] == args.batch:
+                    continue                       # that is the main line itself
+                res["lines"].append(extra_line(args, x, dev))
         if ws == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args, synth.synth_state_dict(uspec, 0),
                                                synth.synth_state_dict(cspec, 0))

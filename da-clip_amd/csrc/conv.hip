@@ -11,6 +11,7 @@ int g_conv2_force = 0;
 // (Ho*Wo <= 1024: the SpatialTransformer level), for in-network sweeps.
 int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
+int g_conv3h_on = getenv("DAC_CONV3H") ? atoi(getenv("DAC_CONV3H")) : 0;
 extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
 extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }
 
@@ -25,7 +26,7 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // (narrow Cout), 15 / 16 / 17 / 18 = v2 1x1 128x256 (GEGLU) / 256x256 / 64x128 / 128x64,
 // 2-stage, 20 = v4 with 32-pixel wave tiles 128x64, 21 = v5 weight-stationary 3x3 (64 -> 64),
 // 22 / 23 = conv_edge.hip init_conv (7x7, Cin 8, Cout 64) / final_conv (3x3, Cout <= 4),
-// 24 = conv_down.hip (4x4 stride-2 Downsample).
+// 24 = conv_down.hip (4x4 stride-2 Downsample), 25 = v6 2-D halo 3x3 (conv3h_kernel).
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -53,6 +54,10 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
       (a.act == ACT_NONE || a.act == ACT_SILU) && a.Cin % (64 / elem_bytes) == 0 && conv3_rw_host(a, 256) > 0 &&
       conv3_rw_host(a, 256) % 64 == 0)
     return 14;
+  if (kh == 3 && (g_conv3_force == 60 || g_conv3_force == 61 || (g_conv3_force < 0 && g_conv3h_on == 2) ||
+                  (g_conv3_force < 0 && g_conv3h_on == 1 && a.Cin >= 128 && !a.res1 && !a.res2 && !a.bbias)) &&
+      conv3h_ok(a, elem_bytes))
+    return 25;
   if (kh == 3 && elem_bytes == 2 && (g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) return 21;
   if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0 && g_conv3_force < 0) {
     const int RW = conv3_rw_host(a, 256);
@@ -112,6 +117,24 @@ bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
   if (a.Cin % a.gna_groups || (a.Cin / a.gna_groups) % 8 || 256 % (a.Cin / 8)) return false;
   if (a.Cout % 128 || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8)) return false;
   return (a.act == ACT_NONE || a.act == ACT_SILU) && (a.Ho * a.Wo) % 64 == 0;
+}
+
+// v6 2-D halo tiles (conv_impl.h conv3h_kernel): 16-bit 3x3 s1 p1, 8-row x 64-column output
+// tiles of one image, whole 64-channel N tiles, 32-channel K chunks, buffer-descriptor DMA (one
+// row pitch, 31-bit byte offsets), the minimal register epilogue, no fused second output.
+bool conv3h_ok(const ConvArgs& a, int elem_bytes) {
+  if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.w_bstride != 0 || a.y2 || a.ln_g || a.lnf_cs ||
+      a.gna_stats)
+    return false;
+  if (a.Cin % 32 || (a.C1 < a.Cin && a.C1 % 32) || a.K != 9 * a.Cin || a.Cout % 64 || a.Wo % 64 || a.Ho % 8)
+    return false;
+  if (!(a.act == ACT_NONE || a.act == ACT_SILU) || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8))
+    return false;
+  if (a.x2 && a.C1 < a.Cin && a.ld2 != a.ld1) return false;       // one row pitch (buffer offsets)
+  const size_t LIM = (size_t)1 << 30;
+  if ((size_t)a.B * a.Hs * a.Ws * a.ld1 * 2 >= LIM || (size_t)a.Cout * a.K * 2 >= LIM) return false;
+  if ((a.ss && (a.ss_ld % 4 || a.Cout % 4 || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
+  return true;
 }
 
 bool conv_res_fusable(const ConvArgs& a) {

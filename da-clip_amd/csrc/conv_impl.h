@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   // (scale, shift) table of this block's image, built in LDS behind the pipeline.
   constexpr bool GNA = (EPK & EPI_GNA) != 0;
   constexpr int EPE = EPK & ~(EPI_LNF | EPI_GNA);
-  static_assert(!LNF || (KH == 1 && KW == 1 && sizeof(T) == 2), "LN fold: 16-bit 1x1 GEMMs");
+  static_assert(!LNF || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPK & EPI_SWAP)), "LN fold: 16-bit 1x1 swapped GEMMs");
   static_assert(!GNA || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPE & EPI_SWAP) && !LNF), "GN in A: 16-bit 1x1 swapped");
   constexpr bool SWAP = (EPE & EPI_SWAP) != 0;
   constexpr bool SLN = (EPE & EPI_LN) != 0 && SWAP;
@@ -510,11 +510,14 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // LN fold: this lane's partial row sums (sum x, sum x^2) of A rows wm*WTM + i*16 + lr over
-  // the K slices it reads (8 of every 32); summed over the four lane groups after the loop.
-  float ls1[LNF ? TM : 1], ls2[LNF ? TM : 1];
+  // LN fold: this lane's partial row sums (sum d, sum d^2, d = x - shift) of A rows
+  // wm*WTM + i*16 + lr over the K slices it reads (8 of every 32); summed over the four lane
+  // groups after the loop. The shift is the row's first element (read from the first K tile in
+  // LDS by all four lane groups of the row), so a row whose mean is many standard deviations
+  // from zero keeps its variance: the moments are taken about a point inside the row.
+  float ls1[LNF ? TM : 1], ls2[LNF ? TM : 1], lsh[LNF ? TM : 1];
 #pragma unroll
-  for (int i = 0; i < (LNF ? TM : 1); ++i) ls1[i] = ls2[i] = 0.f;
+  for (int i = 0; i < (LNF ? TM : 1); ++i) ls1[i] = ls2[i] = lsh[i] = 0.f;
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s);
@@ -603,12 +606,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
           else Mma<T>::run(acc[i][j], fa[i], fb[j]);
         }
       if constexpr (LNF) {
+        if (ks == 0 && kt == 0) {
+          // Element 0 of row wm*WTM + i*16 + lr (logical slot 0), read by all four lane groups.
+#pragma unroll
+          for (int i = 0; i < TM; ++i) lsh[i] = to_f(*reinterpret_cast<const T*>(A + swz(wm * WTM + i * 16 + lr, 0)));
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             float lo, hi;
             unpack2<T>(fa[i][w], lo, hi);
+            lo -= lsh[i];
+            hi -= lsh[i];
             ls1[i] += lo + hi;
             ls2[i] = fmaf(lo, lo, fmaf(hi, hi, ls2[i]));
           }
@@ -623,10 +633,11 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const float t1 = red32_sum(red16_sum(ls1[i])), t2 = red32_sum(red16_sum(ls2[i]));
-      mu[i] = t1 * inv_n;
-      rs[i] = 1.f / sqrtf(fmaxf(t2 * inv_n - mu[i] * mu[i], 0.f) + a.lnf_eps);
+      const float d = t1 * inv_n;                // mean of x - shift
+      mu[i] = lsh[i] + d;
+      rs[i] = 1.f / sqrtf(fmaxf(t2 * inv_n - d * d, 0.f) + a.lnf_eps);
     }
-    if constexpr (SWAP) {
+    {
       // Lane (lr, lg): pixel row i*16 + lr, channels nb .. nb+15 (acc[i][e >> 2][e & 3]).
       const int nb = n0 + wn * WTN + 16 * lg;
       float cs[16];
@@ -636,23 +647,6 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e >> 2][e & 3] = rs[i] * fmaf(-mu[i], cs[e], acc[i][e >> 2][e & 3]);
-    } else {
-      // Lane (lr, lg): pixel rows i*16 + 4lg + r, channel n0 + wn*WTN + j*16 + lr; the moments
-      // of row 4lg + r sit in lane 4lg + r.
-      float cs[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + lr;
-        cs[j] = n < a.Cout ? a.lnf_cs[n] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float m = __shfl(mu[i], 4 * lg + r, 64), q = __shfl(rs[i], 4 * lg + r, 64);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j][r] = q * fmaf(-m, cs[j], acc[i][j][r]);
-        }
     }
   }
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
@@ -1289,6 +1283,10 @@ extern int g_conv3_force;
 extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = built-in
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 extern int g_conv3_buf;       // v4 buffer-resource DMA (FL bit 10); DAC_CONV3_BUF=0 disables
+extern int g_conv3h_on;       // v6 2-D halo kernel: 0 off, 1 measured-faster shapes, 2 all (DAC_CONV3H)
+inline bool conv3h_pick(const ConvArgs& a) {
+  return g_conv3h_on == 2 || (g_conv3h_on == 1 && a.Cin >= 128 && !a.res1 && !a.res2 && !a.bbias);
+}
 
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 bool conv3i_try(const ConvArgs& a, hipStream_t st) {
@@ -1300,6 +1298,8 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
     if (a.x2 && a.C1 < a.Cin && a.ld2 != a.ld1) return false;
     if ((size_t)a.B * a.Hs * a.Ws * a.ld1 * sizeof(T) >= LIM || (size_t)a.Cout * a.K * sizeof(T) >= LIM) return false;
   }
+  if constexpr ((FL & 16) != 0)   // fused res_conv: writes y2 from w2, so both must be given
+    if (!a.y2 || !a.w2) return false;
   if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
     if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
@@ -1514,6 +1514,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
         const int sn = s + NST - 1;                   // stage to issue: (tile + sn/6, sn%6)
         issue(t + (sn / 6) * stride, (sn % 6) / 3, sn % 3, (slot + NST - 1) % NST);
       }
+
       const char* st = ring + slot * STAGE;
       u32x4 fa[NF];
 #pragma unroll
@@ -1545,6 +1546,223 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
     t = tn;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------
+// v6 (3x3, stride 1, pad 1, 16-bit): 2-D halo tiles, one stage per 32-channel chunk.
+// A tile is 8 output rows x 64 columns of one image x 64 output channels; wave w (of 8) owns
+// output row w (64 pixels, TM = 4 interleaved 16-pixel MFMA tiles as in v4) x all 64 channels
+// (swapped operands: weights as the MFMA A operand, so each lane ends with 16 consecutive
+// channels of one pixel and the register epilogue epi_regs16 writes them).
+// One stage holds, for one 32-channel chunk, the whole 10 x 66 input halo of the tile (each
+// input pixel landed in LDS once per chunk, not once per kh as in v4's (chunk, kh) stages)
+// and all 9 weight taps (576 rows): 78 KB, two stages + two epilogue-term slots = 158 KB, one
+// block of 8 waves per CU. Per stage a wave reads 3 x (6 A + 3 x 4 B) fragments and issues 144
+// MFMAs; one barrier per stage (v4: one per 48 MFMAs). LDS-DMA bytes per output are 0.46x v4's
+// (v4's 256 x 64 tiles re-fetch the halo for every kh and the taps for every 256 pixels), which
+// takes the CU's LDS-DMA landing rate off the critical path.
+// Persistent: each block walks tiles of its XCD's contiguous tile range (n-tile fastest, so
+// the blocks of an XCD share halo rows in L2); the next tile's first stage (and its epilogue
+// terms) is DMA'd at the last stage's barrier, under that stage's MFMAs and the epilogue.
+// Buffer-descriptor DMA with out-of-range zero fill for the padding (as v4 FL bit 10).
+constexpr int C3H_RH = 8, C3H_RW = 64, C3H_HWID = C3H_RW + 2;
+constexpr int C3H_NPIX = (C3H_RH + 2) * C3H_HWID;              // 660 halo pixels
+constexpr int C3H_NA = (C3H_NPIX + 15) / 16;                    // 42 A DMA instructions
+constexpr int C3H_NB = 9 * 64 / 16;                             // 36 B DMA instructions
+constexpr int C3H_STAGE = (C3H_NA + C3H_NB) * 1024;             // 79872 B
+constexpr int C3H_SMEM = 2 * C3H_STAGE + 2 * 1024;              // + 2 epilogue-term slots
+static_assert(C3H_SMEM <= 160 * 1024, "v6 LDS");
+inline int conv3h_ntiles(const ConvArgs& a) { return a.B * (a.Ho / C3H_RH) * (a.Wo / C3H_RW) * (a.Cout / 64); }
+
+// FL bit 0 (the default): the stage's LDS-DMA is issued in three parts, one after each kh's
+// MFMAs, instead of all at the stage start, where every wave of the block issues at once right
+// after the barrier (3-8 % faster; starting the blocks out of phase was 5-20 % slower).
+template <typename T, int FL = 1>
+__global__ void __launch_bounds__(512) conv3h_kernel(ConvArgs a, int ntiles) {
+  constexpr int TM = 4, NF = TM + 2, VE = 8, ES = 2;
+  constexpr unsigned OOB = 0x80000000u;
+  using SA = RowSwz<4, TM>;
+  using SB = RowSwz<4, 1>;
+  static_assert(C3H_NPIX % 4 == 0, "A rows: whole permutation groups");
+  __shared__ __attribute__((aligned(1024))) char smem[C3H_SMEM];
+  char* terms = smem + 2 * C3H_STAGE;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int HWo = a.Ho * a.Wo;
+  const int NT = a.Cout / 64, cols = a.Wo / C3H_RW, tiles_img = (a.Ho / C3H_RH) * cols;
+  const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
+  const int x_bytes = a.B * a.Hs * a.Ws * a.ld1 * ES, w_bytes = a.Cout * a.K * ES;
+  const int nchunk = a.Cin / 32;
+
+  // This block's tiles: XCD x's contiguous range [x*ntiles/8, (x+1)*ntiles/8), dealt round-robin
+  // to the blocks of that XCD (blocks b and b+8 share one; speed only).
+  const int nb = gridDim.x, xcd = blockIdx.x & 7, jx = blockIdx.x >> 3, cx = (nb - xcd + 7) >> 3;
+  const int t_beg = (int)((long)xcd * ntiles / 8), t_end = (int)((long)(xcd + 1) * ntiles / 8);
+  int t = t_beg + jx;
+  if (t >= t_end) return;
+
+  struct Tile { int b, oh0, ow0, n0; };
+  auto tile_of = [&](int tt) {
+    Tile o;
+    const int sp = tt / NT;
+    o.n0 = (tt - sp * NT) * 64;
+    o.b = sp / tiles_img;
+    const int r = sp - o.b * tiles_img;
+    o.oh0 = (r / cols) * C3H_RH;
+    o.ow0 = (r - (r / cols) * cols) * C3H_RW;
+    return o;
+  };
+  // Per-tile DMA tables of this wave: A instruction q = wave + 8j (< 42) fills physical halo rows
+  // 16q .. 16q+15 (lane / 4), B instruction q = wave + 8j (< 36) weight rows 16q .. (tap = row / 64).
+  int a_off[6], b_off[5];
+  auto tables = [&](const Tile& tl) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int q = wave + 8 * j;
+      const int P = q * 16 + (lane >> 2);
+      const int R = SA::logical(P);
+      const int hy = R / C3H_HWID, hx = R - hy * C3H_HWID;
+      const int ih = tl.oh0 + hy - 1, iw = tl.ow0 + hx - 1;
+      const bool ok = q < C3H_NA && R < C3H_NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win;
+      const int pix = tl.b * a.Hs * a.Ws + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
+      a_off[j] = ok ? (pix * a.ld1 + SA::slot(R, lane & 3) * VE) * ES : (int)OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int q = wave + 8 * j;
+      const int row = q * 16 + (lane >> 2);
+      const int tap = row >> 6, n = tl.n0 + wperm64(row & 63);
+      b_off[j] = q < C3H_NB ? (int)(((size_t)n * a.K + tap * a.Cin + SB::slot(row, lane & 3) * VE) * ES) : (int)OOB;
+    }
+  };
+  // Pieces [p0, p1) of this wave's 11 DMA instructions (6 A, then 5 B) of stage (tl, c).
+  auto issue_part = [&](const Tile& tl, int c, int slot, int p0, int p1) {
+    char* st = smem + slot * C3H_STAGE;
+    const int ci0 = c * 32;
+    const bool from1 = ci0 < a.C1;
+    const void* xb = from1 ? a.x1 : a.x2;
+    const int soa = (from1 ? ci0 : ci0 - a.C1) * ES;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (j >= p0 && j < p1 && wave + 8 * j < C3H_NA) buf_lds16(xb, x_bytes, st + (wave + 8 * j) * 1024, a_off[j], soa);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+      if (6 + j >= p0 && 6 + j < p1 && wave + 8 * j < C3H_NB)
+        buf_lds16(a.w, w_bytes, st + (C3H_NA + wave + 8 * j) * 1024, b_off[j], ci0 * ES);
+  };
+  auto issue = [&](const Tile& tl, int c, int slot, bool with_terms, int tslot) {
+    issue_part(tl, c, slot, 0, 11);
+    if (with_terms && wave == 0) {                 // lanes 0-15 scale, 16-31 shift, 32-47 bias
+      const int part = lane >> 4, l16 = lane & 15;
+      const float* src = reinterpret_cast<const float*>(a.zero);
+      if (part == 0 && a.ss) src = a.ss + (size_t)tl.b * a.ss_ld + tl.n0 + 4 * l16;
+      else if (part == 1 && a.ss) src = a.ss + (size_t)tl.b * a.ss_ld + a.Cout + tl.n0 + 4 * l16;
+      else if (part == 2 && a.bias) src = a.bias + tl.n0 + 4 * l16;
+      __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(terms + tslot * 1024), 16, 0, 0);
+    }
+  };
+
+  // Fragment offsets (stage-relative): A for (kh, s): halo row (wave + kh) * 66 + TM*lr + s.
+  int aoff[3][NF];
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+    for (int s2 = 0; s2 < NF; ++s2) {
+      const int R = (wave + kh) * C3H_HWID + TM * lr + s2;
+      aoff[kh][s2] = SA::phys(R) * 64 + (SA::slot(R, lg) << 4);
+    }
+  int boff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 16 * j + lr;
+    boff[j] = C3H_NA * 1024 + row * 64 + (SB::slot(row, lg) << 4);   // + tap * 4096
+  }
+
+  // (Residual-row prefetch into registers, as v4 / v5 do, does not fit the register budget.)
+  constexpr bool pre_ok = false;
+  Tile cur = tile_of(t);
+  tables(cur);
+  issue(cur, 0, 0, true, 0);
+  int g = 0, k = 0;
+  while (true) {
+    const int tn = t + cx;
+    const bool has_next = tn < t_end;
+    const Tile nxt = has_next ? tile_of(tn) : cur;
+    f32x4 acc[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    EpiPref<TM> pref;
+    const size_t rowbase = (size_t)cur.b * HWo + (size_t)(cur.oh0 + wave) * a.Wo + cur.ow0;
+    auto pixf = [&](int i) { return rowbase + TM * lr + i; };
+    for (int c = 0; c < nchunk; ++c, ++g) {
+      // Own DMA of stage g landed. At a tile's first stage (after the first tile) the previous
+      // epilogue's 2*TM stores are younger than it and may stay in flight.
+      if (c == 0 && k > 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * TM) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // Next stage: (cur, c + 1), or the next tile's first chunk (with its terms) at the last.
+      const bool nx = c + 1 < nchunk || has_next;
+      const Tile& tn2 = c + 1 < nchunk ? cur : nxt;
+      const int cn = c + 1 < nchunk ? c + 1 : 0;
+      if (c + 1 == nchunk && has_next) tables(nxt);
+      if constexpr ((FL & 1) == 0) {
+        if (nx) issue(tn2, cn, (g + 1) & 1, c + 1 == nchunk, (k + 1) & 1);
+      } else if (nx && c + 1 == nchunk && wave == 0) {   // terms now; the DMA pieces follow the MFMAs
+        const int part = lane >> 4, l16 = lane & 15;
+        const float* src = reinterpret_cast<const float*>(a.zero);
+        if (part == 0 && a.ss) src = a.ss + (size_t)tn2.b * a.ss_ld + tn2.n0 + 4 * l16;
+        else if (part == 1 && a.ss) src = a.ss + (size_t)tn2.b * a.ss_ld + a.Cout + tn2.n0 + 4 * l16;
+        else if (part == 2 && a.bias) src = a.bias + tn2.n0 + 4 * l16;
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)(terms + ((k + 1) & 1) * 1024), 16, 0, 0);
+      }
+      if (c + 1 == nchunk && pre_ok) epi_prefetch<T, TM>(a, cur.n0 + 16 * lg, cur.b, pixf, pref);
+      const char* st = smem + (g & 1) * C3H_STAGE;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        u32x4 fa[NF];
+#pragma unroll
+        for (int s2 = 0; s2 < NF; ++s2) fa[s2] = *reinterpret_cast<const u32x4*>(st + aoff[kh][s2]);
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const char* sb = st + (kh * 3 + kw) * 4096;
+          u32x4 fb[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const u32x4*>(sb + boff[j]);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Mma<T>::run(acc[i][j], fb[j], fa[i + kw]);
+        }
+        if constexpr ((FL & 1) != 0)
+          if (nx) issue_part(tn2, cn, (g + 1) & 1, 4 * kh, kh == 2 ? 11 : 4 * kh + 4);
+      }
+    }
+    // Epilogue of this tile (terms slot k & 1 landed with its first stage).
+    if (pre_ok) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nbch = cur.n0 + 16 * lg;
+    const float* el = reinterpret_cast<const float*>(terms + (k & 1) * 1024) + 16 * lg;
+    float bi[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bi[e] = el[128 + e];
+    if (pre_ok) epi_regs16<T, TM, false, true>(a, acc, bi, nbch, cur.b, pixf, &pref, el);
+    else epi_regs16<T, TM>(a, acc, bi, nbch, cur.b, pixf, nullptr, el);
+    if (!has_next) break;
+    t = tn;
+    cur = nxt;
+    ++k;
+  }
+}
+
+template <typename T>
+void conv3h_launch(const ConvArgs& a, hipStream_t st, int fl = 0) {
+  const int nt = conv3h_ntiles(a);
+  const int grid = nt < 256 ? nt : 256;
+  if (fl == 0) conv3h_kernel<T, 0><<<grid, 512, 0, st>>>(a, nt);
+  else conv3h_kernel<T, 1><<<grid, 512, 0, st>>>(a, nt);
 }
 
 // Kernel shape of the 64 -> 64 3x3 convs: DAC_C3W=<waves>,<TM>,<stages> (tuning), default
@@ -1627,6 +1845,15 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       if (conv3i_try<T, 256, 16, 4, 1, 64, 2, 3, EPI_ALL>(a, st)) return;
   }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2) {
+    // v6 (2-D halo tiles): force 60, or DAC_CONV3H=1 for every shape it takes.
+    // v6 (2-D halo tiles): forces 60 / 61 (without / with the interleaved DMA issue); by default
+    // (DAC_CONV3H=1) the plain convs with Cin >= 128 it measured faster on,
+    // DAC_CONV3H=2 every shape it takes, 0 none.
+    if (((g_conv3_force == 60 || g_conv3_force == 61) ||
+         (g_conv3_force < 0 && conv3h_pick(a))) && conv3h_ok(a, (int)sizeof(T))) {
+      conv3h_launch<T>(a, st, g_conv3_force == 60 ? 0 : 1);
+      return;
+    }
     if ((g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) {
       const int delay = g_conv3_force >= 30 ? (g_conv3_force - 30) * 2 : 6;   // swept: 4-10 best
       conv3w_launch<T>(a, delay, st);

@@ -107,6 +107,8 @@ void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st
 // init_conv (7x7, Cin 8 row-tap layout, Cout 64, bf16 / f16, plain or split-precision weights):
 // weight-stationary persistent kernel (conv_edge.hip).
 bool conv7_ok(const ConvArgs& a);
+// v6 2-D halo 3x3 kernel (conv_impl.h conv3h_kernel) takes this conv (conv.hip).
+bool conv3h_ok(const ConvArgs& a, int elem_bytes);
 template <typename T>
 void conv7(const ConvArgs& a, hipStream_t st);
 // final_conv (3x3, Cin 64 -> Cout <= 4, bf16 / f16, plain or split-precision weights, Wo % 64 == 0):

@@ -15,7 +15,8 @@ from typing import Optional, Sequence
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdaclip_hip.so")
+# DAC_LIB_PATH: an alternative build of the same sources, for A/B measurements only.
+LIB_PATH = os.environ.get("DAC_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdaclip_hip.so")
 
 DAC_F32, DAC_BF16, DAC_FP8, DAC_F16 = 0, 1, 2, 3
 DAC_SRC_F32, DAC_SRC_F16, DAC_SRC_BF16 = 0, 1, 2

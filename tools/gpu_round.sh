@@ -16,8 +16,8 @@ tail -2 $O/tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE FAILED; tail -20 $O/smoke.log; exit 1; }
 timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { echo BENCH FAILED; tail -20 $O/bench.log; exit 1; }
 grep '^{' $O/bench.log > $O/bench.json
-timeout -k 10 600 python -u bench.py --dtype fp32 --modes none > $O/bench_fp32.log 2>&1 || { echo FP32 BENCH FAILED; tail -20 $O/bench_fp32.log; exit 1; }
+timeout -k 10 600 python -u bench.py --dtype fp32 --modes none --lines none > $O/bench_fp32.log 2>&1 || { echo FP32 BENCH FAILED; tail -20 $O/bench_fp32.log; exit 1; }
 grep '^{' $O/bench_fp32.log > $O/bench_fp32.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr --modes none > $O/profrun.log 2>&1 || { echo PROF FAILED; tail -20 $O/profrun.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr --modes none --lines none > $O/profrun.log 2>&1 || { echo PROF FAILED; tail -20 $O/profrun.log; exit 1; }
 python3 tools/kstats.py $(find $O/prof -name "*kernel_stats.csv" | head -1) > $O/kernel_stats_summary.txt
 cut -c1-400 $O/bench.json $O/bench_fp32.json

@@ -2,7 +2,7 @@
 # Per-kernel register / LDS / occupancy table of one source file (device compile only).
 # Usage: tools/kres.sh csrc/conv_k3.hip [name-filter]
 cd "$(dirname "$0")/../da-clip_amd"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c "$1" -o /tmp/kres.o --offload-device-only \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form=1 -fno-slp-vectorize -c "$1" -o /tmp/kres.o --offload-device-only \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import sys, re
 cur = None; rows = []

@@ -15,7 +15,7 @@ for DT in ${PMC_DTYPES:-bf16}; do
     # Per-dispatch counters do not depend on T (every step runs the same kernels on the same
     # shapes), so T=10 keeps the serialized PMC run short.
     DAC_NO_GRAPH=1 timeout -s KILL 600 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_$TAG/p$DT$i -o run -- \
-      python -u bench.py --steps 1 --warmup 0 --T 10 --dtype $DT --modes none --no-cpu-baseline --no-roofline --no-psnr ${BENCH_ARGS} \
+      python -u bench.py --steps 1 --warmup 0 --T 10 --dtype $DT --modes none --lines none --no-cpu-baseline --no-roofline --no-psnr ${BENCH_ARGS} \
       > gpurun_out/pmc_$TAG/p$DT$i.log 2>&1 &
     pid=$!
     while kill -0 $pid 2>/dev/null; do sleep 20; echo "pass $DT $i $(date +%T)" >> gpurun_out/pmc_$TAG/heartbeat; done
