@@ -29,6 +29,18 @@ template <> DEV float silu_t<float>(float x) { return x / (1.f + expf(-x)); }
 template <> DEV float silu_t<bf16>(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 template <> DEV float silu_t<f16>(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
+// 16-bit epilogues fold the per-channel terms once: u = (acc + b) * s + h = acc * s + (b * s + h),
+// and with SiLU they also carry log2(e) in (s, h), so u2 = u * log2(e) comes out of the same fma,
+// 2^-u2 = e^-u needs no extra multiply and silu(u) = u2 * rcp(fma(2^-u2, log2e, log2e)): three
+// VALU + v_exp + v_rcp per value instead of five + the two. Every epilogue path of a kernel uses
+// the same fold, so a row rounds identically whichever path its tile takes (batch invariance).
+constexpr float kL2E = 1.4426950408889634f;
+DEV void epi_fold(float b, float& s, float& h, bool silu) {
+  h = fmaf(b, s, h);
+  if (silu) { s *= kL2E; h *= kL2E; }
+}
+DEV float silu_log2(float u2) { return u2 * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(-u2), kL2E, kL2E)); }
+
 template <int BM, int BN>
 struct EpiLds {
   static constexpr int LDW = BN + 4;                 // floats per LDS row
@@ -216,19 +228,46 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
             acc[i][2 * j2][r] = (acc[i][2 * j2][r] + bi[2 * j2]) * gelu_fast(acc[i][2 * j2 + 1][r] + bi[2 * j2 + 1]);
     }
   } else if (!GEGLU_ONLY && fast) {
+    if constexpr (sizeof(T) == 2) {
+      // Folded terms (epi_fold), SiLU in the log2 domain; the general path below folds alike.
+      const bool silu = a.act == ACT_SILU;
+      float fs[TN], fh[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int j = 0; j < TN; ++j) { fs[j] = sc[j]; fh[j] = sh[j]; epi_fold(bi[j], fs[j], fh[j], silu); }
+      if (silu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          // Explicit fma (and in the general path below): both paths round identically, so a
-          // row's result does not depend on whether its tile spans images (batch invariance).
-          float v = fmaf(acc[i][j][r] + bi[j], sc[j], sh[j]);
-          if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
-          acc[i][j][r] = v;
-        }
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j][r] = silu_log2(fmaf(acc[i][j][r], fs[j], fh[j]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              float v = fmaf(acc[i][j][r], fs[j], fh[j]);
+              if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
+              acc[i][j][r] = v;
+            }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            // Explicit fma (and in the general path below): both paths round identically, so a
+            // row's result does not depend on whether its tile spans images (batch invariance).
+            float v = fmaf(acc[i][j][r] + bi[j], sc[j], sh[j]);
+            if (a.act == ACT_SILU) v = silu_t<T>(v);
+            else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
+            acc[i][j][r] = v;
+          }
+    }
   } else if constexpr ((EPK & EPI_GENERAL) != 0) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -254,12 +293,26 @@ DEV void conv_epilogue_lds(const ConvArgs& a, f32x4 (&acc)[BM / WGM / 16][BN / W
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wn * WTN + j * 16 + lr;
           float v = acc[i][j][r];
-          if (n < a.Cout) {
-            if (a.bias) v += a.bias[n];
-            if (s) v = fmaf(v, s[n] + 1.f, s[a.Cout + n]);
+          if constexpr (sizeof(T) == 2) {
+            // The fast path's fold, element by element (identical rounding).
+            const bool silu = a.act == ACT_SILU;
+            float fs = 1.f, fh = 0.f, fb = 0.f;
+            if (n < a.Cout) {
+              if (a.bias) fb = a.bias[n];
+              if (s) { fs = s[n] + 1.f; fh = s[a.Cout + n]; }
+            }
+            epi_fold(fb, fs, fh, silu);
+            v = fmaf(v, fs, fh);
+            if (silu) v = silu_log2(v);
+            else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
+          } else {
+            if (n < a.Cout) {
+              if (a.bias) v += a.bias[n];
+              if (s) v = fmaf(v, s[n] + 1.f, s[a.Cout + n]);
+            }
+            if (a.act == ACT_SILU) v = silu_t<T>(v);
+            else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
           }
-          if (a.act == ACT_SILU) v = silu_t<T>(v);
-          else if ((EPK & EPI_GELU) && a.act == ACT_GELU) v = gelu_fast(v);
           acc[i][j][r] = v;
         }
       }

@@ -272,15 +272,23 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
     for (int e = 0; e < 16; ++e) gl[e] = a.ln_g[nb + e];
   }
+  // Per channel, once per tile: the folded terms of conv_epi.h epi_fold (bias into the shift,
+  // SiLU in the log2 domain: three VALU + v_exp + v_rcp per value instead of five + the two; the
+  // epilogue's VALU is what the co-resident block's MFMAs must cover). The
+  // activation is a uniform branch around the whole loop, not a per-value select.
+  const bool silu = a.act == ACT_SILU;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) epi_fold(bi[e], sc[e], sh[e], silu);
+  auto body = [&](auto silu_c) {
+  constexpr bool SILU = decltype(silu_c)::value;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const size_t m = pix(i);
     float v[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      float u = fmaf(acc[i][e >> 2][e & 3] + bi[e], sc[e], sh[e]);
-      if (a.act == ACT_SILU) u = silu_t<T>(u);
-      v[e] = u;
+      const float u = fmaf(acc[i][e >> 2][e & 3], sc[e], sh[e]);
+      v[e] = SILU ? silu_log2(u) : u;
     }
     if constexpr (LN) {
       float sm = 0.f;
@@ -328,6 +336,9 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
       store_vec<T>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
     }
   }
+  };
+  if (silu) body(std::true_type{});
+  else body(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------------------
