@@ -52,6 +52,20 @@ template <> DEV void unpack2<f16>(unsigned u, float& lo, float& hi) {
   hi = (float)h[1];
 }
 
+// lo += element 0, hi += element 1 of a packed pair (a residual added to fp32 epilogue values).
+// fp16: one v_fma_mix_f32 per element (the half is converted inside the fma: r * 1 + v, the same
+// single rounding as convert + add) instead of a v_cvt_f32_f16 and a v_add_f32.
+template <typename T> DEV void add_pair(unsigned u, float& lo, float& hi) {
+  float a, b;
+  unpack2<T>(u, a, b);
+  lo += a;
+  hi += b;
+}
+template <> DEV void add_pair<f16>(unsigned u, float& lo, float& hi) {
+  asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel_hi:[1,0,0]" : "+v"(lo) : "v"(u));
+  asm("v_fma_mix_f32 %0, %1, 1.0, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(hi) : "v"(u));
+}
+
 // Load / store VE elements (16 bytes) as fp32 values.
 template <typename T> DEV void load_vec(const T* p, float* out);
 template <> DEV void load_vec<float>(const float* p, float* out) {

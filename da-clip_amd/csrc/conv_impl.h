@@ -312,22 +312,12 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
         const u32x4 r1 = PRE ? pre->v[2 * i + h]
                              : *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res1) + m * a.ldr1 + nb + 8 * h);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {              // element pair -> two floats (no spills)
-          float lo, hi;
-          unpack2<T>(r1[w], lo, hi);
-          v[8 * h + 2 * w] += lo;
-          v[8 * h + 2 * w + 1] += hi;
-        }
+        for (int w = 0; w < 4; ++w) add_pair<T>(r1[w], v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
       }
       if (!PRE && a.res2) {
         const u32x4 r2 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res2) + m * a.ldr2 + nb + 8 * h);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          float lo, hi;
-          unpack2<T>(r2[w], lo, hi);
-          v[8 * h + 2 * w] += lo;
-          v[8 * h + 2 * w + 1] += hi;
-        }
+        for (int w = 0; w < 4; ++w) add_pair<T>(r2[w], v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
       }
       if (!PRE && a.bbias) {
 #pragma unroll
@@ -433,6 +423,29 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
   }
   const int nk = (a.K + BKE - 1) / BKE;
+  // 1x1 with ConvArgs::dbuf: buffer-descriptor DMA. Per-lane byte offsets (pixel row x pitch +
+  // slot; weight row x K + slot) computed once, the K advance in the scalar soffset, rows past
+  // M / Cout (and K tiles past K) as out-of-range offsets that land zeros -- no 64-bit address
+  // arithmetic per DMA instruction.
+  constexpr unsigned OOB = 0x80000000u;
+  constexpr bool DB1 = KH == 1 && KW == 1 && S == 1 && P == 0;
+  int a_bo[DB1 ? AG : 1], b_bo[DB1 ? BG : 1];
+  int x1_bytes = 0, x2_bytes = 0, w_bytes = 0;
+  if constexpr (DB1) {
+    if (a.dbuf) {
+      x1_bytes = a.B * a.Hs * a.Ws * a.ld1 * (int)sizeof(T);
+      x2_bytes = a.x2 ? a.B * a.Hs * a.Ws * a.ld2 * (int)sizeof(T) : 0;
+      w_bytes = a.Cout * a.K * (int)sizeof(T);
+#pragma unroll
+      for (int j = 0; j < AG; ++j) a_bo[j] = a_ih[j] >= 0 ? (a_m[j] * a.ld1 + a_ls[j] * VE) * (int)sizeof(T) : (int)OOB;
+#pragma unroll
+      for (int j = 0; j < BG; ++j) {
+        const int row = (wave * BG + j) * 8 + (lane >> 3);
+        const int n = n0 + (SWAP ? (row & ~63) + wperm64(row & 63) : row);
+        b_bo[j] = n < a.Cout ? (n * a.K + b_ls[j] * VE) * (int)sizeof(T) : (int)OOB;
+      }
+    }
+  }
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE;
@@ -468,6 +481,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
       int ci0 = k0;
       if (a.cwrap && ci0 >= a.cwrap) ci0 -= a.cwrap;
       const bool from1 = ci0 < a.C1;
+      if (a.dbuf) {
+        const int soa = (from1 ? ci0 : ci0 - a.C1) * (int)sizeof(T), sob = k0 * (int)sizeof(T);
+#pragma unroll
+        for (int j = 0; j < AG; ++j)
+          buf_lds16(from1 ? a.x1 : a.x2, from1 ? x1_bytes : x2_bytes, st + (wave * AG + j) * 8 * 128,
+                    kv ? a_bo[j] : (int)OOB, soa);
+#pragma unroll
+        for (int j = 0; j < BG; ++j)
+          buf_lds16(wgt, w_bytes, st + BM * 128 + (wave * BG + j) * 8 * 128, kv ? b_bo[j] : (int)OOB, sob);
+        return;
+      }
       const char* xs = from1 ? reinterpret_cast<const char*>(x1 + ci0) : reinterpret_cast<const char*>(x2 + (ci0 - a.C1));
       const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * sizeof(T);
 #pragma unroll
@@ -700,7 +724,10 @@ inline int conv3_rw(const ConvArgs& a, int BM = 256) {
 // wave-instruction of global_load_lds fills 64 / SLOTS rows; slot swizzle sl ^ f(row) with
 // f(row) = (row >> log2(16 / SLOTS)) & (SLOTS - 1) keeps the 16 rows read by one ds_read_b128
 // lane group on distinct banks.
-template <typename T, int BM, int BN, int WGM, int WGN, int CK>
+// BUF: buffer-descriptor DMA (as v4 FL bit 10): per-lane 32-bit offsets computed once, the chunk
+// and kh advance in the scalar soffset, padding as out-of-range offsets -- no 64-bit address
+// arithmetic per DMA instruction (v3 spent ~3 VALU per MFMA there). One row pitch required.
+template <typename T, int BM, int BN, int WGM, int WGN, int CK, bool BUF = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
@@ -789,10 +816,37 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
         boff[kw][jn][ks] = AROWS * CK + swz(kw * BN + wn * WTN + jn * 16 + lr, ks * 4 + lg);
 
   const int nchunk = a.Cin / BKE;
+  constexpr unsigned OOB = 0x80000000u;
+  int a_bo[BUF ? AG : 1][3], b_bo[BUF ? BG : 1];
+  const int x_bytes = BUF ? a.B * a.Hs * a.Ws * a.ld1 * ES : 0;
+  const int w_bytes = BUF ? a.Cout * a.K * ES : 0;
+  if constexpr (BUF) {
+#pragma unroll
+    for (int j = 0; j < AG; ++j)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+        a_bo[j][kh] = a_pix[j][kh] >= 0 ? (a_pix[j][kh] * a.ld1 + a_ls[j]) * ES : (int)OOB;
+#pragma unroll
+    for (int j = 0; j < BG; ++j) {
+      const int row = (wave * BG + j) * RPI + lane / SLOTS;
+      const int n = n0 + row % BN;
+      b_bo[j] = n < a.Cout ? (int)(((size_t)n * a.K + (row / BN) * a.Cin + b_ls[j]) * ES) : (int)OOB;
+    }
+  }
   auto issue = [&](int c, int kh, int buf) {
     char* st = smem + buf * STAGE;
     const int ci0 = c * BKE;
     const bool from1 = ci0 < a.C1;
+    if constexpr (BUF) {
+      const int soa = (from1 ? ci0 : ci0 - a.C1) * ES, sob = (kh * 3 * a.Cin + ci0) * ES;
+#pragma unroll
+      for (int j = 0; j < AG; ++j)
+        buf_lds16(from1 ? a.x1 : a.x2, x_bytes, st + (wave * AG + j) * RPI * CK, a_bo[j][kh], soa);
+#pragma unroll
+      for (int j = 0; j < BG; ++j)
+        buf_lds16(a.w, w_bytes, st + AROWS * CK + (wave * BG + j) * RPI * CK, b_bo[j], sob);
+      return;
+    }
     const char* xs = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) +
                      (size_t)(from1 ? ci0 : ci0 - a.C1) * ES;
     const size_t ldb = (size_t)(from1 ? a.ld1 : a.ld2) * ES;
@@ -1408,7 +1462,13 @@ struct C3W {
   static constexpr int SMEM = C3W_WBYTES + NWV * NST * STAGE;
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
-template <typename T, int NWV, int TM = 4, int NST = 2>
+// BUF: the halo DMA through a raw buffer descriptor whose base sits one pixel before the input,
+// with every per-lane offset a kernel-lifetime constant (halo column x row pitch + slot) and the
+// segment's row / column start in the scalar soffset; padding lanes (image edges, rows past the
+// halo, rows outside the image, tiles past the wave's range) carry an out-of-range offset the
+// range check lands as zeros. No per-stage address arithmetic and no branches around the DMA
+// (the flat form spent ~55 VALU per stage there). Needs one row pitch (ld2 == ld1 when split).
+template <typename T, int NWV, int TM = 4, int NST = 2, bool BUF = false>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
   using CF = C3W<NWV, TM, NST>;
   constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
@@ -1458,9 +1518,41 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
 #pragma unroll
   for (int j = 0; j < 4; ++j) boff[j] = (16 * j + lr) * 64 + (SB::slot(16 * j + lr, lg) << 4);
 
+  // BUF per-lane constants: byte offset of halo row R = dr (output column ow0 + R - 1, source
+  // column (ow0 >> up) + ((R - 1) >> up)) from the pixel before the segment's first source pixel.
+  constexpr unsigned OOB = 0x80000000u;
+  int boffs[BUF ? NI : 1];
+  const int up = a.up ? 1 : 0;
+  const int x_bytes = BUF ? a.B * a.Hs * a.Ws * a.ld1 * 2 + a.ld1 * 2 : 0;
+  if constexpr (BUF) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      boffs[j] = dr[j] < SEG + 2 ? (int)((((dr[j] - 1) >> up) + 1) * a.ld1 * 2 + dls[j]) : (int)OOB;
+  }
   // Stage (c, kh) of tile tt into ring slot `slot`; tiles past this wave's range load the zero
   // page so every stage issues exactly NI instructions (the counted waits rely on it).
   auto issue = [&](int tt, int c, int kh, int slot) {
+    if constexpr (BUF) {
+      const bool live = tt < t_end;
+      const int rr = live ? tt / segs : 0, ow0 = live ? (tt - rr * segs) * SEG : 0;
+      const int b = rr / a.Ho, oh = rr - b * a.Ho;
+      const int ih = oh + kh - 1;
+      const int ci0 = c * 32;
+      const bool from1 = ci0 < a.C1;
+      const bool row_ok = live && (unsigned)ih < (unsigned)Hin;
+      const int prow = b * a.Hs + (a.up ? (ih >> 1) : ih);
+      const int soff = row_ok ? ((prow * a.Ws + (ow0 >> up)) * a.ld1 + (from1 ? ci0 : ci0 - a.C1)) * 2 : 0;
+      const char* base = reinterpret_cast<const char*>(from1 ? a.x1 : a.x2) - a.ld1 * 2;
+      const bool lpad = ow0 == 0, rpad = ow0 + SEG == a.Wo;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int vo = row_ok ? boffs[j] : (int)OOB;
+        if (j == 0) vo = (lpad && dr[j] == 0) ? (int)OOB : vo;
+        if ((SEG + 1) / 16 == j) vo = (rpad && dr[j] == SEG + 1) ? (int)OOB : vo;
+        buf_lds16(base, x_bytes, ring + slot * STAGE + j * 1024, vo, soff);
+      }
+      return;
+    }
     const bool live = tt < t_end;
     const int rr = live ? tt / segs : 0, ow0 = live ? (tt - rr * segs) * SEG : 0;
     const int b = rr / a.Ho, oh = rr - b * a.Ho;
@@ -1824,11 +1916,39 @@ void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   DAC_C3W(6, 4, 2)
 #undef DAC_C3W
   const int ntiles = a.B * a.Ho * (a.Wo >> 6);
-  conv3w_kernel<T, C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+  // Buffer-descriptor DMA when the input has one row pitch and 31-bit byte offsets.
+  static const int buf_env = getenv("DAC_C3W_BUF") ? atoi(getenv("DAC_C3W_BUF")) : 1;
+  const bool buf = buf_env && (a.C1 >= a.Cin || !a.x2 || a.ld2 == a.ld1) &&
+                   (size_t)a.B * a.Hs * a.Ws * a.ld1 * 2 + a.ld1 * 2 < ((size_t)1 << 31);
+  if (buf)
+    conv3w_kernel<T, C3W_WAVES, 4, 2, true><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+  else
+    conv3w_kernel<T, C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+}
+
+// v3 launch, buffer-descriptor DMA when the input has one row pitch and 30-bit byte offsets.
+template <typename T, int BM, int BN, int WGM, int WGN, int CK>
+void conv3_launch(const ConvArgs& a, dim3 g, int RW, hipStream_t st) {
+  constexpr size_t LIM = (size_t)1 << 30;
+  const bool buf = g_conv3_buf && (a.C1 >= a.Cin || !a.x2 || a.ld2 == a.ld1) &&
+                   (size_t)a.B * a.Hs * a.Ws * a.ld1 * sizeof(T) < LIM && (size_t)a.Cout * a.K * sizeof(T) < LIM;
+  if (buf) conv3_kernel<T, BM, BN, WGM, WGN, CK, true><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
+  else conv3_kernel<T, BM, BN, WGM, WGN, CK><<<g, 64 * WGM * WGN, 0, st>>>(a, RW);
 }
 
 template <typename T, int KH, int KW, int S, int P>
-void conv_dispatch(const ConvArgs& a, hipStream_t st) {
+void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
+  // 1x1 GEMMs: buffer-descriptor DMA when the input has one row pitch and every byte offset
+  // fits 31 bits (ConvArgs::dbuf; DAC_CONV3_BUF=0 disables it with the 3x3 forms).
+  ConvArgs a = a0;
+  a.dbuf = 0;
+  if constexpr (KH == 1 && KW == 1 && S == 1 && P == 0) {
+    constexpr size_t LIM = (size_t)1 << 31;
+    const size_t es = sizeof(T);
+    a.dbuf = g_conv3_buf && (!a.x2 || a.C1 >= a.Cin || a.ld2 == a.ld1) && !a.up &&
+             (size_t)a.B * a.Hs * a.Ws * a.ld1 * es < LIM && (!a.x2 || (size_t)a.B * a.Hs * a.Ws * a.ld2 * es < LIM) &&
+             (size_t)a.Cout * a.K * es < LIM;
+  }
   // A fused second output is only requested after conv_res_fusable(a) said the v4 path takes it;
   // no path below may return without writing it.
   if (a.y2 && !(KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2 && conv_res_fusable(a))) abort();
@@ -1940,20 +2060,20 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st) {
       // (< 2 blocks per CU, the 32x32 level) keep the 8-wave block.
       if (a.Cout <= 64 && conv3_rw(a, 128) > 0) {
         dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 63) / 64, 1);
-        conv3_kernel<T, 128, 64, 2, 2, 64><<<g, 256, 0, st>>>(a, conv3_rw(a, 128));
+        conv3_launch<T, 128, 64, 2, 2, 64>(a, g, conv3_rw(a, 128), st);
         return;
       }
       if (a.Cout <= 64) {
         dim3 g(a.B * a.Ho * a.Wo / 256, (a.Cout + 63) / 64, 1);
-        conv3_kernel<T, 256, 64, 4, 2, 128><<<g, 512, 0, st>>>(a, RW);
+        conv3_launch<T, 256, 64, 4, 2, 128>(a, g, RW, st);
         return;
       }
       if (conv3_rw(a, 128) > 0) {
         dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 127) / 128, 1);
         if ((long)g.x * g.y >= 512)
-          conv3_kernel<T, 128, 128, 2, 2, 64><<<g, 256, 0, st>>>(a, conv3_rw(a, 128));
+          conv3_launch<T, 128, 128, 2, 2, 64>(a, g, conv3_rw(a, 128), st);
         else
-          conv3_kernel<T, 128, 128, 2, 4, 128><<<g, 512, 0, st>>>(a, conv3_rw(a, 128));
+          conv3_launch<T, 128, 128, 2, 4, 128>(a, g, conv3_rw(a, 128), st);
         return;
       }
     }

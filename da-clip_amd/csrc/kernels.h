@@ -73,6 +73,9 @@ struct ConvArgs {
   const float* gna_g;
   const float* gna_b;
   int gna_groups;
+  // Set by the dispatcher, never by callers: the 1x1 GEMM kernels (conv2_kernel) issue their
+  // LDS-DMA through buffer descriptors (one row pitch, 31-bit byte offsets).
+  int dbuf;
   int gna_nb;
   float gna_eps;
 };
