@@ -233,9 +233,16 @@ template <int N> DEV void fkv_wait(int n) {
   }
 }
 
-template <typename T, int QG>
-__global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restrict__ qkv, T* o, int L,
-                                                              int H, float scale) {
+//  * PRE (q prescaled by scale * log2(e), so scores come out in log2 units): the S^T MFMAs
+//    start from C = -m (m the query's reference max) instead of 0, so p = 2^s' needs no
+//    subtraction; m is only moved when some score of the wave passes it by more than 2^FKV_TAU
+//    (p <= 2^8 fits T and the fp32 sums), the first chunk setting it. Exact: every p and every
+//    rescale uses the same m, and the final 1/sum cancels it.
+constexpr float FKV_TAU = 8.f;
+template <typename T, int QG, int NW = FKV_NW, bool PRE = false>
+__global__ void __launch_bounds__(64 * NW) flash_kv_kernel(const T* __restrict__ qkv, T* o, int L,
+                                                          int H, float scale) {
+  static_assert(NW == 8 || NW == 16, "8 waves (two per SIMD) or 16 (four per SIMD)");
   constexpr int D = 32;
   extern __shared__ __attribute__((aligned(1024))) char fkv_smem[];
   char* sK = fkv_smem;
@@ -255,34 +262,38 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
   int qi[QG];
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    qi[g] = bx * (FKV_NW * 16 * QG) + wave * (16 * QG) + g * 16 + lr;
+    qi[g] = bx * (NW * 16 * QG) + wave * (16 * QG) + g * 16 + lr;
     qf[g] = *reinterpret_cast<const u32x4*>(base + (size_t)qi[g] * ld + h * D + lg * 8);
   }
-  // K / V DMA: instruction n fills keys 16n..16n+15 (1 KB); chunk c = instructions 8c..8c+7,
-  // wave w issues instruction 8c + w of K and of V (2 per wave per chunk).
+  // K / V DMA: instruction n fills keys 16n..16n+15 (1 KB); chunk c = instructions 8c..8c+7.
+  // 8 waves: wave w issues instruction 8c + w of K and of V (2 per wave per chunk); 16 waves:
+  // waves 0-7 issue K's, waves 8-15 V's (1 per wave per chunk).
   const int NC = L >> 7;
+  constexpr int PER = NW == 8 ? 2 : 1;                // DMAs per wave per chunk
   {
     const int kl = lane >> 2, ch = lane & 3;
     for (int c = 0; c < NC; ++c) {
-      const int nn = 8 * c + wave;
+      const int nn = 8 * c + (wave & 7);
       const int key = 16 * nn + kl;
       const T* src = base + (size_t)key * ld + h * D + 8 * (ch ^ fkv_swz(key));
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + H * D),
-                                       (__attribute__((address_space(3))) void*)(sK + nn * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * H * D),
-                                       (__attribute__((address_space(3))) void*)(sV + nn * 1024), 16, 0, 0);
+      if (NW == 8 || wave < 8)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + H * D),
+                                         (__attribute__((address_space(3))) void*)(sK + nn * 1024), 16, 0, 0);
+      if (NW == 8 || wave >= 8)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2 * H * D),
+                                         (__attribute__((address_space(3))) void*)(sV + nn * 1024), 16, 0, 0);
     }
   }
 
   // Row sums of P come out of the PV MFMAs: a third O^T tile whose A operand is all ones
   // (every row = sum over keys of P[q][key], in the same rounded P the numerator uses), so
   // no per-score add and no cross-lane reduction at the end.
-  f32x4 oacc[QG][2], lacc[QG];
+  f32x4 oacc[QG][2], lacc[QG], mneg[QG];
   float mrun[QG];
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    oacc[g][0] = oacc[g][1] = lacc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mrun[g] = -INFINITY;
+    oacc[g][0] = oacc[g][1] = lacc[g] = mneg[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mrun[g] = PRE ? 0.f : -INFINITY;
   }
   const uint32_t one2 = std::is_same<T, f16>::value ? 0x3C003C00u : 0x3F803F80u;   // 1.0 in T, twice
   const u32x4 ones = u32x4{one2, one2, one2, one2};
@@ -290,44 +301,53 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
   typedef short v4i16 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+  int first = 1;                                 // opaque to the compiler: no peeled copy of chunk 0
   for (int c = 0; c < NC; ++c) {
-    fkv_wait<14>(2 * (NC - 1 - c));             // this wave's DMAs of chunk c have landed
+    asm volatile("" : "+s"(first));
+    fkv_wait<7 * PER>(PER * (NC - 1 - c));      // this wave's DMAs of chunk c have landed
     __builtin_amdgcn_s_barrier();                // ... and every other wave's
     asm volatile("" ::: "memory");
     const int kb = c * 128;
-    u32x4 kf[8];
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
+    auto kload = [&](int mi) -> u32x4 {
       const int key = kb + mi * 16 + lr;
-      kf[mi] = *reinterpret_cast<const u32x4*>(sK + key * 64 + ((lg ^ fkv_swz(key)) << 4));
-    }
+      return *reinterpret_cast<const u32x4*>(sK + key * 64 + ((lg ^ fkv_swz(key)) << 4));
+    };
     // V^T fragments: step st (32 keys), d tile dm: rows = keys, lane (4q+p) addresses key
     // kb + 32st + 4lg + q (+16), columns dm*16 + 4p .. +3.
-    u32x4 vf[4][2];
+    auto vload = [&](int st, int dm) -> u32x4 {
+      uint32_t w[4];
 #pragma unroll
-    for (int st = 0; st < 4; ++st)
-#pragma unroll
-      for (int dm = 0; dm < 2; ++dm) {
-        uint32_t w[4];
-#pragma unroll
-        for (int hi = 0; hi < 2; ++hi) {
-          const int key = kb + 32 * st + 16 * hi + 4 * lg + (lr >> 2);
-          const int byte = (dm * 16 + 4 * (lr & 3)) * 2;          // 8-byte column group
-          const int off = key * 64 + ((((byte >> 4) ^ fkv_swz(key)) << 4) | (byte & 15));
-          const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(sV + off));
-          const uint2 u = __builtin_bit_cast(uint2, r);
-          w[2 * hi] = u.x;
-          w[2 * hi + 1] = u.y;
-        }
-        vf[st][dm] = u32x4{w[0], w[1], w[2], w[3]};
+      for (int hi = 0; hi < 2; ++hi) {
+        const int key = kb + 32 * st + 16 * hi + 4 * lg + (lr >> 2);
+        const int byte = (dm * 16 + 4 * (lr & 3)) * 2;          // 8-byte column group
+        const int off = key * 64 + ((((byte >> 4) ^ fkv_swz(key)) << 4) | (byte & 15));
+        const v4i16 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(sV + off));
+        const uint2 u = __builtin_bit_cast(uint2, r);
+        w[2 * hi] = u.x;
+        w[2 * hi + 1] = u.y;
       }
+      return u32x4{w[0], w[1], w[2], w[3]};
+    };
+    // 8 waves: the chunk's K / V fragments are read once and serve all QG groups; 16 waves
+    // (128 VGPRs) re-read them per group instead of holding 64 registers of them.
+    constexpr bool HOIST = NW == 8;
+    u32x4 kf[HOIST ? 8 : 1], vf[HOIST ? 4 : 1][2];
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) kf[mi] = kload(mi);
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int dm = 0; dm < 2; ++dm) vf[st][dm] = vload(st, dm);
+    }
 #pragma unroll
     for (int g = 0; g < QG; ++g) {
+      if constexpr (!HOIST) asm volatile("" ::: "memory");
       f32x4 s[8];
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
-        s[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
-        Mma<T>::run(s[mi], kf[mi], qf[g]);
+        s[mi] = mneg[g];
+        Mma<T>::run(s[mi], HOIST ? kf[mi] : kload(mi), qf[g]);
       }
       float tmax = s[0][0];
 #pragma unroll
@@ -336,19 +356,46 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
         for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[mi][r]);
       tmax = red16_max(tmax);
       tmax = red32_max(tmax);
-      const float mnew = fmaxf(mrun[g], tmax * cs);
+      if constexpr (PRE) {
+        // s = score - m (log2 units). Rare case (the first chunk, or a score more than 2^TAU
+        // above m): move m up to the chunk's max, rescale, and redo the S^T MFMAs from the new
+        // -m, so both cases end in the same p = 2^s with no per-score subtraction.
+        if (first || __any(tmax > FKV_TAU)) {
+          const float sh = first ? tmax : fmaxf(tmax, 0.f);
+          if (!first) {
+            const float corr = __builtin_amdgcn_exp2f(-sh);
+            lacc[g] *= corr;
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
+            for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+          }
+          mrun[g] += sh;
+          mneg[g] = f32x4{-mrun[g], -mrun[g], -mrun[g], -mrun[g]};
+          asm volatile("" ::: "memory");         // K re-read from LDS: kf need not stay live
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
-      // Rescale only when some query's running max moved (exact: otherwise corr == 1).
-      if (DAC_FKV_SKIP == 0 || __any(mnew != mrun[g])) {
-        const float corr = __builtin_amdgcn_exp2f(mrun[g] - mnew);
-        lacc[g] *= corr;
+          for (int mi = 0; mi < 8; ++mi) {
+            s[mi] = mneg[g];
+            Mma<T>::run(s[mi], kload(mi), qf[g]);
+          }
+        }
 #pragma unroll
-        for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(s[mi][r]);
+      } else {
+        const float mnew = fmaxf(mrun[g], tmax * cs);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(fmaf(s[mi][r], cs, -mnew));
+        // Rescale only when some query's running max moved (exact: otherwise corr == 1).
+        if (DAC_FKV_SKIP == 0 || __any(mnew != mrun[g])) {
+          const float corr = __builtin_amdgcn_exp2f(mrun[g] - mnew);
+          lacc[g] *= corr;
+#pragma unroll
+          for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+        }
+        mrun[g] = mnew;
       }
-      mrun[g] = mnew;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
         typename Vec8<T>::t pb;
@@ -359,10 +406,11 @@ __global__ void __launch_bounds__(64 * FKV_NW) flash_kv_kernel(const T* __restri
         }
         const u32x4 pbu = __builtin_bit_cast(u32x4, pb);
 #pragma unroll
-        for (int dm = 0; dm < 2; ++dm) Mma<T>::run(oacc[g][dm], vf[st][dm], pbu);
+        for (int dm = 0; dm < 2; ++dm) Mma<T>::run(oacc[g][dm], HOIST ? vf[st][dm] : vload(st, dm), pbu);
         Mma<T>::run(lacc[g], ones, pbu);
       }
     }
+    first = 0;
   }
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
@@ -537,24 +585,65 @@ __global__ void __launch_bounds__(64 * FKR_NW) flash_kr_kernel(const T* __restri
 // 1: the K/V-ring kernel is the dispatcher's choice for the L <= 1024 shapes (DAC_FLASH_KR).
 int g_flash_kr = getenv("DAC_FLASH_KR") ? atoi(getenv("DAC_FLASH_KR")) : 0;
 
-template <typename T, int QG>
-static void fkv_optin() {
+// 1: the 16-wave flash_kv (four waves per SIMD, two query groups each) is the dispatcher's
+// choice for the K/V-resident shapes (DAC_FKV16).
+int g_fkv16 = getenv("DAC_FKV16") ? atoi(getenv("DAC_FKV16")) : 0;
+
+template <typename T, int QG, int NW, bool PRE>
+static void fkv_launch(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
   // > 64 KB of dynamic LDS must be opted into, once per (kernel, device).
   static std::atomic<uint64_t> done{0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev >= 64) dev = 63;
   const uint64_t bit = 1ull << dev;
-  if (done.load(std::memory_order_acquire) & bit) return;
-  (void)hipFuncSetAttribute((const void*)flash_kv_kernel<T, QG>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-  done.fetch_or(bit, std::memory_order_acq_rel);
+  if (!(done.load(std::memory_order_acquire) & bit)) {
+    (void)hipFuncSetAttribute((const void*)flash_kv_kernel<T, QG, NW, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              131072);
+    done.fetch_or(bit, std::memory_order_acq_rel);
+  }
+  const dim3 g(L / (NW * 16 * QG), H, B);
+  flash_kv_kernel<T, QG, NW, PRE><<<g, 64 * NW, (size_t)L * 128, st>>>((const T*)qkv, (T*)o, L, H, scale);
 }
 
 // variant: 0 = the dispatcher's choice (g_flash_old = DAC_FLASH_OLD selects the staged-tile
 // kernel process-wide, g_flash_kr = DAC_FLASH_KR the K/V-ring one), 1 = the staged-tile kernel,
-// 2 = the K/V-ring kernel (16-bit, L % 64 == 0). Passed explicitly by the op-level test
-// hook, so no global state is toggled per call.
+// 2 = the K/V-ring kernel (16-bit, L % 64 == 0), 3 = the 16-wave K/V-resident kernel (16-bit,
+// L % 256 == 0, L <= 1024). Passed explicitly by the op-level test hook, so no global state is
+// toggled per call. scale == 0: q was prescaled by 32^-0.5 * log2(e) (the engine's 16-bit
+// q|k|v weights), scores are already in log2 units.
 template <typename T>
 void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale, int variant, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    const bool pre = scale == 0.f;
+    const bool kv = L % 128 == 0 && L <= 1024 && variant == 0 && !g_flash_old && !g_flash_kr;
+    if (L % 256 == 0 && L <= 1024 && (variant == 3 || (kv && (pre || g_fkv16)))) {
+      // 16 waves x 2 query groups: the same 512 queries per block as the 8-wave QG = 4 kernel,
+      // with four waves per SIMD to overlap one wave's S -> max -> exp -> PV chain; one query
+      // group per wave (256 queries per block) when 512 would leave CUs idle. The log2-domain
+      // (prescaled q) kernels are built only in this form and the QG = 1 8-wave one (the
+      // 8-wave QG = 4 form spills with the extra -m operands).
+      const bool two = L % 512 == 0 && (long)(L / 512) * H * B >= 256;
+      if (pre) {
+        if (two) fkv_launch<T, 2, 16, true>(qkv, o, B, L, H, scale, st);
+        else fkv_launch<T, 1, 16, true>(qkv, o, B, L, H, scale, st);
+      } else {
+        if (two) fkv_launch<T, 2, 16, false>(qkv, o, B, L, H, scale, st);
+        else fkv_launch<T, 1, 16, false>(qkv, o, B, L, H, scale, st);
+      }
+      return;
+    }
+    if (kv) {
+      // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
+      // fills the chip, else 2 (or 1).
+      if (pre) fkv_launch<T, 1, FKV_NW, true>(qkv, o, B, L, H, scale, st);
+      else if (L % 512 == 0 && (long)(L / 512) * H * B >= 256) fkv_launch<T, 4, FKV_NW, false>(qkv, o, B, L, H, scale, st);
+      else if (L % 256 == 0) fkv_launch<T, 2, FKV_NW, false>(qkv, o, B, L, H, scale, st);
+      else fkv_launch<T, 1, FKV_NW, false>(qkv, o, B, L, H, scale, st);
+      return;
+    }
+  }
+  // The other kernels take the multiplier: prescaled scores need 1 / log2(e).
+  if (scale == 0.f) scale = 0.6931471805599453f;
   if constexpr (sizeof(T) == 2) {
     if (L % 64 == 0 && (variant == 2 || (variant == 0 && g_flash_kr && !g_flash_old && L % 128 == 0 && L <= 1024))) {
       // K/V-ring kernel: 2 query groups per wave (128 queries per block) while that leaves
@@ -565,25 +654,6 @@ void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale
       } else {
         dim3 g(L / 64, H, B);
         flash_kr_kernel<T, 1><<<g, 64 * FKR_NW, 0, st>>>((const T*)qkv, (T*)o, L, H, scale);
-      }
-      return;
-    }
-    if (L % 128 == 0 && L <= 1024 && variant == 0 && !g_flash_old) {
-      // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
-      // fills the chip, else 2 (or 1).
-      const size_t smem = (size_t)L * 128;
-      if (L % 512 == 0 && (long)(L / 512) * H * B >= 256) {
-        fkv_optin<T, 4>();
-        dim3 g(L / 512, H, B);
-        flash_kv_kernel<T, 4><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
-      } else if (L % 256 == 0) {
-        fkv_optin<T, 2>();
-        dim3 g(L / 256, H, B);
-        flash_kv_kernel<T, 2><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
-      } else {
-        fkv_optin<T, 1>();
-        dim3 g(L / 128, H, B);
-        flash_kv_kernel<T, 1><<<g, 64 * FKV_NW, smem, st>>>((const T*)qkv, (T*)o, L, H, scale);
       }
       return;
     }

@@ -403,7 +403,10 @@ struct Packer {
     return f;
   }
   // Row-concatenation of several [Oi][I] linears (q | k | v) into one GEMM.
-  ConvW concat(const std::vector<std::string>& keys, int O, int I, std::vector<float>* keep = nullptr) {
+  // The first block's rows are multiplied by `scale0` before rounding (q prescaled for the
+  // attention kernel's log2-domain softmax).
+  ConvW concat(const std::vector<std::string>& keys, int O, int I, std::vector<float>* keep = nullptr,
+               float scale0 = 1.f) {
     ConvW cw;
     cw.cout = O * (int)keys.size(); cw.cin = cw.cin_real = I;
     std::vector<float> p;
@@ -413,6 +416,8 @@ struct Packer {
       if (!w) { ok = false; continue; }
       p.insert(p.end(), w->v.begin(), w->v.end());
     }
+    if (ok && scale0 != 1.f)
+      for (size_t i = 0; i < (size_t)O * I; ++i) p[i] *= scale0;
     if (ok) {
       cw.w = upload_T(p, keys[0]);
       make_fp8(cw, p, cw.cout, I);
@@ -631,7 +636,8 @@ struct UNetNet {
               bool self_ok = false; ConvW qkv2, o2; const float *n2w = nullptr, *n2b = nullptr;
               int cc_off = 0;
               // norm1 folded into q|k|v (16-bit handles, not fp8).
-              ConvW qkv_f; const float* qkv_cs = nullptr; };
+              ConvW qkv_f; const float* qkv_cs = nullptr;
+              bool q_pre = false; };   // q rows of qkv / qkv_f prescaled (see load_attn)
   struct Attn { bool st = false; LA la; ST s; };
   struct Level { RB b1, b2; Attn at; ConvW samp; };
 
@@ -703,7 +709,11 @@ struct UNetNet {
     s.pin = P.conv(f + "proj_in.weight", C, C, 1, 1, f + "proj_in.bias");
     const std::string b = f + "transformer_blocks.0.";
     std::vector<float> pq;
-    s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C, &pq);
+    // 16-bit handles: q comes out of its GEMM already times 32^-0.5 * log2(e) (one rounding, as
+    // for q itself), so the attention kernel's scores are in log2 units (flash_kv PRE).
+    s.q_pre = sizeof(T) == 2;
+    s.qkv = P.concat({b + "attn1.to_q.weight", b + "attn1.to_k.weight", b + "attn1.to_v.weight"}, C, C, &pq,
+                     s.q_pre ? (float)(1.4426950408889634 / std::sqrt(32.0)) : 1.f);
     s.o = P.linear(b + "attn1.to_out.0.weight", C, C, b + "attn1.to_out.0.bias");
     s.ff1 = P.geglu(b + "ff.net.0.proj.weight", b + "ff.net.0.proj.bias", 4 * C, C);
     if (sizeof(T) == 2 && !P.fp8 && fold_on(1)) {
@@ -986,7 +996,7 @@ struct UNetNet {
     }
     T* o = r.alloc<T>(M * C);
     r.flops += 4.0 * B * (double)L * L * C;     // QK^T and PV
-    if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, 0.17677669529663687f, r.st);
+    if (!r.dry) flash_attn_d32<T>(qkv, o, B, L, C / 32, s.q_pre ? 0.f : 0.17677669529663687f, r.st);
     emu_round<T>(r, o, C, M, C);
     T* h2 = r.alloc<T>(M * C);
     Epi e;

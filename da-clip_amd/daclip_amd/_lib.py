@@ -23,6 +23,7 @@ DAC_SRC_F32, DAC_SRC_F16, DAC_SRC_BF16 = 0, 1, 2
 DAC_POSTERIOR, DAC_SDE = 0, 1
 DAC_COSINE, DAC_LINEAR, DAC_CONSTANT = 0, 1, 2
 DAC_E_MISSING, DAC_E_KEY = -3, -2
+DAC_ATTN_Q_PRESCALED = 8
 
 EXPORTS = ["dac_create", "dac_destroy", "dac_set_weight", "dac_finalize_weights",
            "dac_encode_image", "dac_encode_text", "dac_degradation_probs", "dac_unet_forward",

@@ -3,7 +3,8 @@ heads of d = 32, softmax(q k^T * 32^-0.5) v) through the C ABI hook dac_op_atten
 a plain PyTorch fp32 reference of the same op on the same bf16 / fp16 (or fp32) inputs.
 
 Covers the K/V-resident kernel (bf16, L % 128 == 0, L <= 1024: the 32x32 UNet levels at 256^2)
-in each of its query-group configurations, the K/V-ring kernel (variant 2, L % 64 == 0), the
+in each of its query-group configurations and its 16-wave form (variant 3, L % 256 == 0), the
+K/V-ring kernel (variant 2, L % 64 == 0), the
 staged-tile kernel it falls back to (ragged L, fp32, or forced), and that they agree."""
 import ctypes
 
@@ -44,11 +45,20 @@ def test_attention_16bit_matches_fp32_reference(B, L, H, dt):
     tdt, code = (torch.bfloat16, _lib.DAC_BF16) if dt == "bf16" else (torch.float16, _lib.DAC_F16)
     qkv = (torch.randn(B * L, 3 * H * 32, device="cuda", generator=g) * 1.5).to(tdt)
     ref = _ref(qkv, B, L, H)
-    for variant in ((0, 1, 2) if L % 64 == 0 else (0, 1)):
-        out = _run(qkv, B, L, H, code, variant).float()
-        err = (out - ref).abs().max().item() / ref.abs().max().item()
-        # 16-bit P and output rounding: measured ~3e-3 (bf16); fp16 8x finer.
-        assert err < (1e-2 if dt == "bf16" else 2e-3), (variant, err)
+    variants = (0, 1, 2) if L % 64 == 0 else (0, 1)
+    if L % 256 == 0 and L <= 1024:
+        variants += (3,)
+    # The engine's 16-bit q|k|v weights emit q already times 32^-0.5 log2(e) (one rounding):
+    # the kernels then take scores in log2 units (DAC_ATTN_Q_PRESCALED).
+    pre = qkv.float()
+    pre.view(B * L, 3, H * 32)[:, 0] *= 32 ** -0.5 * 1.4426950408889634
+    pre = pre.to(tdt)
+    for variant in variants:
+        for flag, q in ((0, qkv), (_lib.DAC_ATTN_Q_PRESCALED, pre)):
+            out = _run(q, B, L, H, code, variant | flag).float()
+            err = (out - ref).abs().max().item() / ref.abs().max().item()
+            # 16-bit P and output rounding: measured ~3e-3 (bf16); fp16 8x finer.
+            assert err < (1e-2 if dt == "bf16" else 2e-3), (variant, flag, err)
 
 
 def test_attention_kernels_agree_and_handle_peaky_scores():
@@ -65,10 +75,27 @@ def test_attention_kernels_agree_and_handle_peaky_scores():
     a = _run(qkv, B, L, H, _lib.DAC_BF16, 0).float()
     b = _run(qkv, B, L, H, _lib.DAC_BF16, 1).float()
     c = _run(qkv, B, L, H, _lib.DAC_BF16, 2).float()
-    assert torch.isfinite(a).all() and torch.isfinite(c).all()
+    d = _run(qkv, B, L, H, _lib.DAC_BF16, 3).float()
+    assert torch.isfinite(a).all() and torch.isfinite(c).all() and torch.isfinite(d).all()
     assert (a - ref).abs().max().item() / ref.abs().max().item() < 1e-2
     assert (a - b).abs().max().item() / ref.abs().max().item() < 1e-2
     assert (c - ref).abs().max().item() / ref.abs().max().item() < 1e-2
+    assert (d - ref).abs().max().item() / ref.abs().max().item() < 1e-2
+    # Prescaled q: the log2-domain kernels move their reference max when a chunk passes it by
+    # more than 2^8 (here: most chunks), and must equal the unscaled result.
+    # The reference takes the same rounded q (at these logits, 300+ in log2 units, bf16's
+    # rounding of q * 32^-0.5 log2(e) alone moves scores by ~1).
+    f = 32 ** -0.5 * 1.4426950408889634
+    pre = qkv.float()
+    pre.view(B, L, 3, H, 32)[:, :, 0] *= f
+    pre = pre.to(torch.bfloat16)
+    back = pre.float()
+    back.view(B, L, 3, H, 32)[:, :, 0] /= f
+    ref_pre = _ref(back, B, L, H)
+    for variant in (0, 3):
+        e = _run(pre, B, L, H, _lib.DAC_BF16, variant | _lib.DAC_ATTN_Q_PRESCALED).float()
+        assert torch.isfinite(e).all()
+        assert (e - ref_pre).abs().max().item() / ref_pre.abs().max().item() < 1e-2, variant
 
 
 def test_attention_fp32_matches_reference():

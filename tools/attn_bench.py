@@ -12,11 +12,16 @@ from daclip_amd import _lib  # noqa: E402
 it = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 L_ = _lib.lib()
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-for (B, L, H) in [(8, 1024, 16), (8, 1024, 8)]:
-    qkv = torch.randn(B * L, 3 * H * 32, device="cuda").to(torch.bfloat16)
-    out = torch.empty(B * L, H * 32, device="cuda", dtype=torch.bfloat16)
-    for variant in (0, 1, 2):
-        args = (ctypes.c_void_p(qkv.data_ptr()), ctypes.c_void_p(out.data_ptr()), B, L, H, _lib.DAC_BF16, variant, st)
+for (B, L, H), (tdt, code) in [(s, d) for s in [(8, 1024, 16), (8, 1024, 8)]
+                               for d in [(torch.float16, _lib.DAC_F16), (torch.bfloat16, _lib.DAC_BF16)]]:
+    qkv = torch.randn(B * L, 3 * H * 32, device="cuda").to(tdt)
+    out = torch.empty(B * L, H * 32, device="cuda", dtype=tdt)
+    pre = qkv.float()
+    pre.view(B * L, 3, H * 32)[:, 0] *= 32 ** -0.5 * 1.4426950408889634
+    pre = pre.to(tdt)
+    for variant in (0, 1, 2, 3, 8, 11):          # 8 | v: q prescaled (the engine's form)
+        q = pre if variant & 8 else qkv
+        args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(out.data_ptr()), B, L, H, code, variant, st)
         for _ in range(3):
             L_.dac_op_attention(*args)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -27,4 +32,4 @@ for (B, L, H) in [(8, 1024, 16), (8, 1024, 8)]:
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / it
         fl = 4.0 * B * H * L * L * 32
-        print(f"B={B} L={L} H={H} variant={variant}: {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
+        print(f"{str(tdt)[6:]} B={B} L={L} H={H} variant={variant}: {us:8.1f} us  {fl / us / 1e6:7.1f} TF/s", flush=True)
