@@ -747,6 +747,8 @@ struct UNetNet {
     return a;
   }
 
+  // Split-precision (hi | lo) edge weights: bf16 handles (and fp8, whose activations are bf16).
+  static constexpr bool split_edges = std::is_same<T, bf16>::value;
   void load(Packer<T>& P) {
     ss_total = cc_total = n_st = 0;
     if (degra) prompt = P.f32("prompt", {1, tdim});
@@ -755,8 +757,11 @@ struct UNetNet {
     // init_conv, final_conv and final_res_block.res_conv keep split-precision weights in bf16
     // handles: their bf16 rounding error alone moved the T=100 restore by up to ~1e-3 dB
     // (measured with the DAC_EMU_* probe); together they are ~1.4 % of the FLOPs.
-    init_conv = P.conv_dual("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "",
-                            sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0);
+    // f16 handles keep plain weights there: f16's own weight rounding (2^-12 relative) is that of
+    // the activations it produces, and the split doubles the init conv's MFMAs.
+    const int kwp7 = sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0;
+    init_conv = split_edges ? P.conv_dual("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", kwp7)
+                            : P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", false, kwp7);
     if (half) {
       half_down = P.conv("downsample.weight", nf, nf, 4, 4, "downsample.bias");
       half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias");
@@ -800,7 +805,7 @@ struct UNetNet {
     mid1 = load_rb(P, "mid_block1.", mid, mid);
     mid_attn = load_attn(P, "mid_attn.", mid, imgctx);
     mid2 = load_rb(P, "mid_block2.", mid, mid);
-    fin = load_rb(P, "final_res_block.", 2 * nf, nf, /*dual_res=*/true);
+    fin = load_rb(P, "final_res_block.", 2 * nf, nf, /*dual_res=*/split_edges);
     final_conv = P.conv_dual("final_conv.weight", cfg.out_nc, nf, 3, 3, "final_conv.bias");
   }
 
