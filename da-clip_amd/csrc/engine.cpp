@@ -892,7 +892,10 @@ struct UNetNet {
   const void* linattn(Run& r, const LA& la, const void* x, int C, int B, int H, int W) {
     RoleScope rs(g_role == R_MID ? R_MID : R_LA);
     const size_t M = (size_t)B * H * W;
-    if (C == 64 || C == 128) {
+    // C = 256 (the 64x64 level) takes the fused pair too on 16-bit handles (DAC_LA256=0: the
+    // unfused chain below, for A/B).
+    static const bool la256 = !getenv("DAC_LA256") || atoi(getenv("DAC_LA256")) != 0;
+    if (C == 64 || C == 128 || (C == 256 && sizeof(T) == 2 && la256)) {
       // Fused (linattn.hip): context pass over x, then one apply pass x -> y (LN, q projection
       // and softmax, per-image to_out, its LayerNorm and the Residual).
       T* weff = r.alloc<T>((size_t)B * C * 128);

@@ -290,7 +290,7 @@ struct LaCfg {
   static constexpr int SL = RB / 16;                     // 16-byte slots per x row
   static constexpr int XT = TP * RB;                     // one x tile
   static constexpr int QV = C / 4 / VE;                  // x vectors per thread (4 thr / px)
-  static constexpr bool WREG = ES == 2;                  // weights cached in registers
+  static constexpr bool WREG = ES == 2 && C <= 128;      // weights cached in registers (C = 256: L2)
   static constexpr int SMEM = 2 * XT + 4 * 64 * 4;      // x tiles + per-wave rescale scratch
   DEV static int swz(int row, int s) {                   // x tile slot swizzle
     const int f = SL >= 16 ? (row & 15) : SL == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
@@ -556,7 +556,7 @@ template <typename T> DEV int la_qcol(int qc) {  // LDS column of q channel qc i
   }
 }
 
-template <typename T>
+template <typename T, int NJ>   // NJ = C / 64 output (channel, row) pairs per thread, 256 at a time
 __global__ void __launch_bounds__(256) la_combine_weff(const float* __restrict__ part, const float* __restrict__ wout,
                                                        T* __restrict__ weff, int C, int nc, float inv_hw) {
   constexpr int NG = 8, PER = 16;                // chunk groups x chunks per group (la_chunks() <= 128)
@@ -578,9 +578,9 @@ __global__ void __launch_bounds__(256) la_combine_weff(const float* __restrict__
     for (int r = 0; r < 4; ++r) v[k][r] = ok ? pc[(hd0 + r) * 32 + e] : 0.f;
     sv[k] = (ok && e < 4) ? pc[4096 + hd0 + e] : 0.f;
   }
-  float4 wv[2][8];                               // output i = tid + 256 j: channel i >> 2
+  float4 wv[NJ][8];                              // output i = tid + 256 j: channel i >> 2
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int i = tid + 256 * j;
     const float* w = wout + (size_t)(i < C * 4 ? i >> 2 : 0) * 128 + h * 32;
 #pragma unroll
@@ -635,7 +635,7 @@ __global__ void __launch_bounds__(256) la_combine_weff(const float* __restrict__
   __syncthreads();
   // 2. W_eff rows: thread -> (output channel c, row r).
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int i = tid + 256 * j;
     if (i >= C * 4) break;
     const int c = i >> 2, r = i & 3;
@@ -906,13 +906,22 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
   float* part = ws;
   if (C == 64)
     la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
-  else
+  else if (C == 128)
     la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
+  else if constexpr (sizeof(T) == 2)
+    la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
+  else
+    __builtin_trap();
   // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
   // stored without the 1/HW and la_apply applies it to the fp32 accumulators (wscale).
   const float inv_hw = 1.f / (float)HW;
   const bool hw_late = std::is_same<T, f16>::value;
-  la_combine_weff<T><<<dim3(32, B), 256, 0, st>>>(part, wout, (T*)weff, C, nc, hw_late ? 1.f : inv_hw);
+  if (C == 64)
+    la_combine_weff<T, 1><<<dim3(32, B), 256, 0, st>>>(part, wout, (T*)weff, C, nc, hw_late ? 1.f : inv_hw);
+  else if (C == 128)
+    la_combine_weff<T, 2><<<dim3(32, B), 256, 0, st>>>(part, wout, (T*)weff, C, nc, hw_late ? 1.f : inv_hw);
+  else
+    la_combine_weff<T, 4><<<dim3(32, B), 256, 0, st>>>(part, wout, (T*)weff, C, nc, hw_late ? 1.f : inv_hw);
   const float wscale = hw_late ? inv_hw : 1.f;
   static int ncu = 0;
   if (!ncu) {
@@ -921,15 +930,19 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 8)
       ncu = 256;
   }
-  // Resident blocks per CU (LDS-bound): 4 for bf16 C = 64 (32 KB of weights each), else 2.
-  const int per_cu = (C == 64 && sizeof(T) == 2) ? 4 : 2;
+  // Resident blocks per CU (LDS-bound): 4 for 16-bit C = 64 (32 KB of weights each), 1 for
+  // C = 256 (128 KB), else 2.
+  const int per_cu = C == 256 ? 1 : (C == 64 && sizeof(T) == 2) ? 4 : 2;
   int nb = (per_cu * ncu + B - 1) / B;
   nb = std::max(1, std::min(nb, (HW + 63) / 64));
   if (C == 64)
     la_apply<T, 64><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
                                                  (T*)y, HW, 1e-5f, wscale);
-  else
+  else if (C == 128)
     la_apply<T, 128><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                  (T*)y, HW, 1e-5f, wscale);
+  else if constexpr (sizeof(T) == 2)
+    la_apply<T, 256><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
                                                   (T*)y, HW, 1e-5f, wscale);
 }
 
