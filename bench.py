@@ -45,6 +45,8 @@ for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
     KERNEL_SYMBOL[(321, _dt)] = f"_ZN3dac13conv3w_kernelI{_m}Li8ELi4ELi2EEEvNS_8ConvArgsEii"
     KERNEL_SYMBOL[(306, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
     KERNEL_SYMBOL[(307, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
+# fp8 handles: class 340 = conv3q (e4m3 64 -> 64 ResBlock block2 on the block-scaled MFMA).
+KERNEL_SYMBOL[(340, "fp8")] = "_ZN3dac13conv3q_kernelIDF16bEEvNS_8ConvArgsEPKhS3_ii"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -83,8 +85,9 @@ def parse():
                    help="fp16 (default) = IEEE half storage on the f16 MFMA, fp32 accumulation: the "
                         "16-bit mode that holds the north-star 1e-3 dB PSNR bar; bf16 = the same kernels "
                         "with bf16 storage (BASELINE configs[1] names bf16; same bytes and MFMA rate, 8x "
-                        "coarser rounding, measured -6.5e-3 dB, reported under 'modes'); fp8 = e4m3 MX "
-                        "GEMMs (BASELINE configs[4]); fp32 = parity mode")
+                        "coarser rounding, measured -6.5e-3 dB, reported under 'modes'); fp8 = bf16 kernels with "
+                        "the 64->64 ResBlock block2 convs and the ViT GEMMs on e4m3 MX operands (BASELINE "
+                        "configs[4]); fp32 = parity mode")
     p.add_argument("--modes", default="bf16",
                    help="comma-separated extra dtypes measured after the main line on 1 GPU (throughput "
                         "+ PSNR vs the reference), reported under 'modes'; 'none' to skip")
@@ -96,14 +99,14 @@ def parse():
                         "main workload; 'none' to skip")
     p.add_argument("--kernel-id", type=int, default=None,
                    help="conv class timed for the roofline (kh*100 + variant; default 312 = 3x3 "
-                        "interleaved-row v4 tiles, 330 = the fp8 3x3 kernel for --dtype fp8)")
+                        "interleaved-row v4 tiles, 340 = conv3q, the e4m3 ResBlock block2 kernel, for --dtype fp8)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the PSNR-vs-reference sample")
     p.add_argument("--cpu-steps", type=int, default=5, help="UNet steps in the CPU sample (>= 5)")
     a = p.parse_args()
     if a.kernel_id is None:
-        a.kernel_id = 330 if a.dtype == "fp8" else 312
+        a.kernel_id = 340 if a.dtype == "fp8" else 312
     wild = a.model == "wild-ir"
     a.batch = a.batch or (2 if wild else 8)
     a.res = a.res or (512 if wild else 256)

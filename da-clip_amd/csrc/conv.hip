@@ -124,7 +124,7 @@ bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
 // row pitch, 31-bit byte offsets), the minimal register epilogue, no fused second output.
 bool conv3h_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.w_bstride != 0 || a.y2 || a.ln_g || a.lnf_cs ||
-      a.gna_stats)
+      a.gna_stats || a.ys8 || a.xs8)
     return false;
   if (a.Cin % 32 || (a.C1 < a.Cin && a.C1 % 32) || a.K != 9 * a.Cin || a.Cout % 64 || a.Wo % 64 || a.Ho % 8)
     return false;
@@ -148,8 +148,23 @@ bool conv_res_fusable(const ConvArgs& a) {
   return kok && conv3_rw_host(a, 128) > 0 && conv3_rw_host(a, 128) % 32 == 0;
 }
 
+// fp8-output block1 (ConvArgs::ys8): mirrors the two dispatcher branches that take it — the
+// weight-stationary 64 -> 64 conv (buffer DMA form) and the fused-res_conv v4 256x64 tiles.
+bool conv_q8out_ok(const ConvArgs& a0) {
+  ConvArgs a = a0;
+  a.ys8 = reinterpret_cast<uint8_t*>(&a);          // (asked before the tensor exists)
+  if (a.Cout != 64 || a.ldy != 64 || a.res1 || a.res2 || a.bbias || a.xs8 || g_conv3_force >= 0) return false;
+  if (!a.y2) {
+    const bool buf = (a.C1 >= a.Cin || !a.x2 || a.ld2 == a.ld1) &&
+                     (size_t)a.B * a.Hs * a.Ws * a.ld1 * 2 + a.ld1 * 2 < ((size_t)1 << 31);
+    return conv3w_ok(a) && buf;
+  }
+  return conv_res_fusable(a) && conv_variant(a, 3, 2) == 12;
+}
+
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {
+  if (a.xs8) abort();                              // e4m3 inputs: conv3q only
   if (kh == 3 && kw == 3 && s == 1 && p == 1) conv_dispatch<T, 3, 3, 1, 1>(a, st);
   else if (kh == 1 && kw == 1 && s == 1 && p == 0) conv_dispatch<T, 1, 1, 1, 0>(a, st);
   else if (kh == 4 && kw == 4 && s == 2 && p == 1) conv_dispatch<T, 4, 4, 2, 1>(a, st);

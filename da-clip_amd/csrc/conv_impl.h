@@ -230,9 +230,37 @@ DEV void epi_prefetch(const ConvArgs& a, int nb, int b, const PixOf& pix, EpiPre
   }
 }
 
+typedef short short2_t __attribute__((ext_vector_type(2)));
+// fp8 output of a register epilogue (ConvArgs::ys8): the lane's 16 values of pixel m, channels
+// nb .. nb+15, become e4m3 under one E8M0 exponent per 32-channel half (lanes lg and lg ^ 1 hold
+// one half: a permlane16 max). The exponent is the smallest with |v| / 2^e <= 440 (a margin below
+// e4m3's 448, so the product rounding of max / 440 can never push a value past it); one 16-byte
+// store of the bytes, one byte store of the exponent from the half's first lane.
+DEV void q8_store(const ConvArgs& a, size_t m, int nb, const float (&v)[16]) {
+  float mx = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) mx = fmaxf(mx, fabsf(v[e]));
+  mx = red16_max(mx);
+  const uint32_t u = __float_as_uint(mx * (1.f / 440.f));
+  int ex = (int)(u >> 23) - 127 + ((u & 0x7fffffu) != 0u);
+  ex = ex < -126 ? -126 : (ex > 126 ? 126 : ex);
+  const float sc = __uint_as_float((uint32_t)(ex + 127) << 23);
+  u32x4 q;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    short2_t s = {0, 0};
+    s = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(s, v[4 * w], v[4 * w + 1], sc, false);
+    s = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(s, v[4 * w + 2], v[4 * w + 3], sc, true);
+    q[w] = __builtin_bit_cast(uint32_t, s);
+  }
+  *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(a.y) + m * a.ldy + nb) = q;
+  if ((nb & 16) == 0) a.ys8[m * (a.Cout >> 5) + (nb >> 5)] = (uint8_t)(ex + 127);
+}
+
 // PRE: operands come from epi_prefetch and the conv has no bbias / res2 / (ss with res1) —
 // the epilogue then issues no loads at all, so it never waits for in-flight DMA.
-template <typename T, int TM, bool LN = false, bool PRE = false, class PixOf>
+// Q8: the output is e4m3 + exponents (q8_store) instead of T.
+template <typename T, int TM, bool LN = false, bool PRE = false, bool Q8 = false, class PixOf>
 DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
                     const PixOf& pix, const EpiPref<TM>* pre = nullptr, const float* ssl = nullptr) {
   T* y = reinterpret_cast<T*>(a.y);
@@ -323,8 +351,9 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[8 * h + e] += bb[8 * h + e];
       }
-      store_vec<T>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
+      if constexpr (!Q8) store_vec<T>(y + m * a.ldy + nb + 8 * h, v + 8 * h);
     }
+    if constexpr (Q8) q8_store(a, m, nb, v);
   }
   };
   if (silu) body(std::true_type{});
@@ -1322,8 +1351,11 @@ conv3i_kernel(ConvArgs a, int RW) {
     const float* el = reinterpret_cast<const float*>(smem + ST * STAGE) + 16 * lg;   // LDS terms
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = el[128 + e];
-    if (pre_ok) epi_regs16<T, TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
-    else epi_regs16<T, TM>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
+    // FL bit 12: fp8 output (ConvArgs::ys8, q8_store) — the fp8 handles' block1 with a fused
+    // res_conv, whose y2 stays 16-bit.
+    constexpr bool Q8 = (FL & 4096) != 0;
+    if (pre_ok) epi_regs16<T, TM, false, true, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
+    else epi_regs16<T, TM, false, false, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
     if constexpr (RES) {
       // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
       T* y2 = reinterpret_cast<T*>(a.y2);
@@ -1468,7 +1500,7 @@ struct C3W {
 // halo, rows outside the image, tiles past the wave's range) carry an out-of-range offset the
 // range check lands as zeros. No per-stage address arithmetic and no branches around the DMA
 // (the flat form spent ~55 VALU per stage there). Needs one row pitch (ld2 == ld1 when split).
-template <typename T, int NWV, int TM = 4, int NST = 2, bool BUF = false>
+template <typename T, int NWV, int TM = 4, int NST = 2, bool BUF = false, bool Q8 = false>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
   using CF = C3W<NWV, TM, NST>;
   constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
@@ -1644,7 +1676,7 @@ __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles
     // Epilogue: tile i of lane (lr, lg) is pixel m0 + TM*lr + i, channels nb .. nb+15. The
     // prefetched operands landed once at most the next tile's first stage (NI DMA) is pending.
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NI) : "memory");
-    epi_regs16<T, TM, false, true>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, &pref);
+    epi_regs16<T, TM, false, true, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)m0 + TM * lr + i; }, &pref);
     if (tn >= t_end) break;
     t = tn;
   }
@@ -1904,7 +1936,7 @@ template <typename T>
 void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   const C3WCfg c = c3w_cfg(a.Wo % 64 == 0 && (long)a.B * a.Ho * (a.Wo / 64) < 2L * 256 * C3W_WAVES);
 #define DAC_C3W(NW_, TM_, NS_)                                                                 \
-  if (c.nwv == NW_ && c.tm == TM_ && c.nst == NS_ && a.Wo % (16 * TM_) == 0) {                  \
+  if (!a.ys8 && c.nwv == NW_ && c.tm == TM_ && c.nst == NS_ && a.Wo % (16 * TM_) == 0) {       \
     const int ntiles = a.B * a.Ho * (a.Wo / (16 * TM_));                                        \
     conv3w_kernel<T, NW_, TM_, NS_><<<conv3w_blocks(ntiles, NW_), 64 * NW_, 0, st>>>(a, ntiles, delay); \
     return;                                                                                     \
@@ -1920,7 +1952,10 @@ void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   static const int buf_env = getenv("DAC_C3W_BUF") ? atoi(getenv("DAC_C3W_BUF")) : 1;
   const bool buf = buf_env && (a.C1 >= a.Cin || !a.x2 || a.ld2 == a.ld1) &&
                    (size_t)a.B * a.Hs * a.Ws * a.ld1 * 2 + a.ld1 * 2 < ((size_t)1 << 31);
-  if (buf)
+  if (a.ys8) {                                      // fp8 output (conv_q8out_ok): buffer DMA form only
+    if (!buf) abort();
+    conv3w_kernel<T, C3W_WAVES, 4, 2, true, true><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
+  } else if (buf)
     conv3w_kernel<T, C3W_WAVES, 4, 2, true><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
   else
     conv3w_kernel<T, C3W_WAVES, 4, 2><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
@@ -2029,6 +2064,11 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         if constexpr (sizeof(T) == 2) {
           // Buffer-resource DMA (FL bit 10) first; the flat-address form takes what it rejects.
           const int nb = g_conv3_buf ? 1024 : 0;
+          if (a.ys8) {                                // fp8 output (conv_q8out_ok): fused-res tiles only
+            if (a.y2 && a.Cout == 64 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024 | 4096>(a, st)) return;
+            if (a.y2 && a.Cout == 64 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 4096>(a, st)) return;
+            abort();
+          }
           if (a.y2) {
             if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;

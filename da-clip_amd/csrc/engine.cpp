@@ -62,6 +62,11 @@ static int fold_mask() {
   return e ? atoi(e) : kFoldDefault;
 }
 static bool fold_on(int bit) { return (fold_mask() & bit) != 0; }
+// DAC_Q8=0: fp8 handles keep the 16-bit ResBlock pairs (A/B switch for the e4m3 block2 path).
+static bool q8_on() {
+  static const bool on = !getenv("DAC_Q8") || atoi(getenv("DAC_Q8")) != 0;
+  return on;
+}
 static bool no_res_fuse() {
   static const int v = getenv("DAC_NO_RES_FUSE") ? atoi(getenv("DAC_NO_RES_FUSE")) : 0;
   return v != 0;
@@ -246,7 +251,31 @@ struct Packer {
   DevPool& pool;
   WStore& ws;
   bool fp8 = false;                    // also build the e4m3 weights of every eligible layer
+  bool q8 = false;                     // fp8 handles' UNet: e4m3 64 -> 64 ResBlock block2 weights
   static constexpr int VE = sizeof(T) == 2 ? 8 : 4;
+
+  // conv3q weights of a 3x3 64 -> 64 conv from its packed [64][3][3][64] fp32 values: e4m3 bytes
+  // [64][9][64] with one E8M0 exponent per (output channel, tap, 32-channel half), the smallest
+  // with max |w| / 2^e <= 448.
+  void make_q8c3(ConvW& cw, const std::vector<float>& p) {
+    if (!q8 || sizeof(T) != 2 || cw.kh != 3 || cw.kw != 3 || cw.cin != 64 || cw.cout != 64 || cw.kwp ||
+        p.size() != (size_t)64 * 576)
+      return;
+    std::vector<uint8_t> w8((size_t)64 * 576), s8((size_t)64 * 18);
+    for (int n = 0; n < 64; ++n)
+      for (int t = 0; t < 9; ++t)
+        for (int h = 0; h < 2; ++h) {
+          const float* src = &p[(size_t)n * 576 + t * 64 + 32 * h];
+          float mx = 0.f;
+          for (int c = 0; c < 32; ++c) mx = std::max(mx, std::fabs(src[c]));
+          int e = mx > 0.f ? (int)std::ceil(std::log2((double)mx / 448.0)) : 0;
+          e = std::min(126, std::max(-126, e));
+          s8[(size_t)n * 18 + t * 2 + h] = (uint8_t)(127 + e);
+          for (int c = 0; c < 32; ++c) w8[(size_t)n * 576 + t * 64 + 32 * h + c] = f2e4m3_host(std::ldexp(src[c], -e));
+        }
+    cw.q8w = (const uint8_t*)pool.upload(w8.data(), w8.size());
+    cw.q8s = (const uint8_t*)pool.upload(s8.data(), s8.size());
+  }
 
   // fp8 copy of a packed [O][K] weight (conv8.hip): K padded to a multiple of 128 with zeros,
   // one E8M0 exponent per (row, 64-k block) chosen so the block's largest |w| / 2^e <= 448.
@@ -456,10 +485,9 @@ Profiler::~Profiler() {
   for (auto e : ev) (void)hipEventDestroy(e);
 }
 
-template <typename T>
-void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,
-               int B, int Hs, int Ws, int up, int stride, int pad, void* y, int ldy,
-               const Epi& e) {
+// The kernel arguments of a conv_call (the fused res_conv's fields included when requested).
+static ConvArgs conv_args(const Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,
+                          int B, int Hs, int Ws, int up, int stride, int pad, void* y, int ldy, const Epi& e) {
   ConvArgs a{};
   a.x1 = x1; a.x2 = x2; a.ld1 = ld1; a.ld2 = ld2; a.C1 = C1; a.Cin = cw.cin;
   a.Hs = Hs; a.Ws = Ws; a.up = up; a.B = B;
@@ -485,13 +513,24 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   a.lnf_cs = e.lnf_cs; a.lnf_n = e.lnf_n; a.lnf_eps = e.lnf_eps;
   a.gna_stats = e.gna_stats; a.gna_g = e.gna_g; a.gna_b = e.gna_b; a.gna_groups = e.gna_groups;
   a.gna_nb = e.gna_nb; a.gna_eps = e.gna_eps;
+  a.ys8 = e.ys8; a.xs8 = e.xs8;
+  if (e.fuse1x1) {
+    a.w2 = e.fuse1x1->w; a.w2_dual = e.fuse1x1->dual; a.bias2 = e.fuse1x1->b; a.y2 = e.y2; a.ldy2 = e.ldy2;
+  }
+  return a;
+}
+
+template <typename T>
+void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const void* x2, int ld2,
+               int B, int Hs, int Ws, int up, int stride, int pad, void* y, int ldy,
+               const Epi& e) {
+  ConvArgs a = conv_args(r, cw, x1, ld1, C1, x2, ld2, B, Hs, Ws, up, stride, pad, y, ldy, e);
   const double M = (double)B * a.Ho * a.Wo;
   double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
   Profiler* p = r.prof;
   const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
   bool fused = false;
   if (e.fuse1x1) {
-    a.w2 = e.fuse1x1->w; a.w2_dual = e.fuse1x1->dual; a.bias2 = e.fuse1x1->b; a.y2 = e.y2; a.ldy2 = e.ldy2;
     fused = sizeof(T) == 2 && !use8 && a.w2 && cw.kh == 3 && stride == 1 && pad == 1 && !up &&
             e.fuse1x1->cout == cw.cout && e.fuse1x1->cin == cw.cin && conv_res_fusable(a);
     if (!fused) {
@@ -503,7 +542,8 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     }
   }
   r.flops += fl;
-  const int cls = cw.kh * 100 + (use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
+  // Class 340: the fp8 ResBlock block2 (conv3q); an fp8-output block1 keeps its kernel's class.
+  const int cls = cw.kh * 100 + (a.xs8 ? 40 : use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
   const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == cls);
   if (r.dry) {
     if (timed) p->used++;
@@ -513,14 +553,21 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   // (Dry runs carry no zero page; the engine chose these paths with the same predicates.)
   if (a.lnf_cs && !conv_lnf_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: LN fold requested on a shape without a folding kernel");
   if (a.gna_stats && !conv_gna_ok(a, (int)sizeof(T))) throw Error(DAC_E_STATE, "conv: GroupNorm A path requested on a shape without such a kernel");
+  if (a.ys8 && !conv_q8out_ok(a)) throw Error(DAC_E_STATE, "conv: fp8 output requested on a shape without such a kernel");
+  if (a.xs8 && !(sizeof(T) == 2 && cw.q8w && conv3q_ok(a))) throw Error(DAC_E_STATE, "conv: fp8 input on a layer without fp8 weights / kernel");
   if (a.Cin % (16 / (int)sizeof(T)) || (a.x2 == nullptr && a.C1 < a.Cin))
     throw Error(DAC_E_ARG, "conv: bad channel layout");
   if (timed) {
     if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
     HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
   }
-  if (use8) conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
-  else conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+  if (a.xs8) {
+    if constexpr (sizeof(T) == 2) conv3q<T>(a, cw.q8w, cw.q8s, r.st);
+  } else if (use8) {
+    conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
+  } else {
+    conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+  }
   emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
   if (fused) emu_round<T>(r, e.y2, e.ldy2, (size_t)M, cw.cout);
   if (timed) {
@@ -537,9 +584,10 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
       p->lflops.push_back(fl);
     }
     // Algorithmic HBM bytes: every operand touched once (input, weights, output, residuals).
-    const double es = sizeof(T);
-    p->bytes += es * ((double)B * Hs * Ws * cw.cin_real + (double)cw.cout * cw.kh * cw.kw * cw.cin +
-                      M * cw.cout * (1 + (e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0)));
+    // (e4m3 tensors: 1 byte per value + 2 exponent bytes per pixel; e4m3 weights 1 byte.)
+    const double es = sizeof(T), ei = a.xs8 ? 1 + 2.0 / 64 : es, eo = a.ys8 ? 1 + 2.0 / 64 : es;
+    p->bytes += ei * B * Hs * Ws * cw.cin_real + (a.xs8 ? 1 : es) * cw.cout * cw.kh * cw.kw * cw.cin +
+                M * cw.cout * (eo + es * ((e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0)));
   }
 }
 
@@ -673,7 +721,9 @@ struct UNetNet {
     rb.mw = P.f32(p + "mlp.1.weight", {2 * dout, tdim});
     rb.mb = P.f32(p + "mlp.1.bias", {2 * dout});
     rb.c1 = P.conv(p + "block1.proj.weight", dout, din, 3, 3);
-    rb.c2 = P.conv(p + "block2.proj.weight", dout, dout, 3, 3);
+    std::vector<float> p2;
+    rb.c2 = P.conv(p + "block2.proj.weight", dout, dout, 3, 3, "", false, 0, P.q8 ? &p2 : nullptr);
+    if (P.q8 && dout == 64) P.make_q8c3(rb.c2, p2);
     if (din != dout) {
       rb.has_res = true;
       rb.res = dual_res ? P.conv_dual(p + "res_conv.weight", dout, din, 1, 1)
@@ -875,6 +925,33 @@ struct UNetNet {
       // res_conv rides along in block1's conv kernel (same input; conv_call falls back to a
       // separate launch when the kernel cannot take it).
       e1.fuse1x1 = &rb.res; e1.y2 = rr; e1.ldy2 = rb.dout;
+    }
+    if (rb.c2.q8w && q8_on()) {
+      // fp8 handles: h = block1's output lives only as block2's input, so block1's epilogue
+      // writes it as e4m3 + per-(pixel, 32-channel) exponents and block2 runs on the block-scaled
+      // MFMA (conv3q.hip). Shapes without both kernels keep the 16-bit pair.
+      ConvArgs q = conv_args(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h1, 64, e1);
+      q.zero = &q;                                // (dry runs carry no zero page)
+      ConvArgs q2 = q;
+      q2.x1 = h1; q2.x2 = nullptr; q2.xs8 = reinterpret_cast<const uint8_t*>(&q); q2.ld1 = q2.C1 = q2.Cin = 64;
+      q2.K = 576; q2.ss = nullptr; q2.res1 = res; q2.ldr1 = rb.has_res ? rb.dout : Ca; q2.y2 = nullptr; q2.w2 = nullptr;
+      q2.ys8 = nullptr;
+      if (conv_q8out_ok(q) && conv3q_ok(q2)) {
+        uint8_t* h8 = r.alloc<uint8_t>(M * 64);
+        uint8_t* hs = r.alloc<uint8_t>(M * 2);
+        e1.ys8 = hs;
+        conv_call<T>(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h8, 64, e1);
+        if (rb.has_res) {
+          if (no_res_fuse()) conv_call<T>(r, rb.res, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 0, rr, rb.dout, Epi());
+          res = rr;
+          ldr = rb.dout;
+        }
+        T* o = r.alloc<T>(M * rb.dout);
+        Epi e2;
+        e2.act = ACT_SILU; e2.res1 = res; e2.ldr1 = ldr; e2.xs8 = hs;
+        conv_call<T>(r, rb.c2, h8, 64, 64, nullptr, 0, B, H, W, 0, 1, 1, o, rb.dout, e2);
+        return o;
+      }
     }
     conv_call<T>(r, rb.c1, xa, Ca, Ca, xb, Cb, B, H, W, 0, 1, 1, h1, rb.dout, e1);
     if (rb.has_res) {
@@ -1344,8 +1421,14 @@ class EngineT : public Engine {
   void finalize(WStore& ws) override {
     HIP_OK(hipSetDevice(dev));
     Packer<T> P{pool, ws};
-    P.fp8 = fp8;
+    // fp8 handles: the UNet runs the 16-bit kernels with its 64 -> 64 ResBlock block2 convs on
+    // e4m3 (q8: conv3q.hip, fed by e4m3 block1 epilogues); the ViT's GEMMs take e4m3 MX weights
+    // (conv8.hip). (conv8 on the UNet's layers measured 1.2-3.5x slower than their 16-bit
+    // kernels: it quantizes activations in its A loader.)
+    P.q8 = fp8;
     if (unet) unet->load(P);
+    P.q8 = false;
+    P.fp8 = fp8;
     if (vit) vit->load(P, ws);
     if (!ws.missing.empty()) {
       std::string m = "Missing key(s) in state_dict: ";

@@ -68,6 +68,10 @@ struct ConvW {
   const uint8_t* w8 = nullptr;
   const uint8_t* ws8 = nullptr;
   int kp8 = 0;
+  // fp8 handles, the 64 -> 64 ResBlock block2 convs: e4m3 weights [64][9 taps][64] + E8M0
+  // exponents [64][9][2] (per output channel, tap, 32-channel half) for conv3q.hip.
+  const uint8_t* q8w = nullptr;
+  const uint8_t* q8s = nullptr;
 };
 
 // ----------------------------------------------------------------------------- run context
@@ -137,6 +141,10 @@ struct Epi {
   int gna_groups = 0;
   int gna_nb = 0;                // > 0: gna_stats holds per-block group sums (ConvArgs::gna_nb)
   float gna_eps = 1e-6f;
+  // fp8 ResBlock pair (ConvArgs::ys8 / xs8): ys8 = the output is e4m3 (ldy bytes per pixel) with
+  // these exponents; xs8 = the input x1 is e4m3 with these exponents (conv3q, weights cw.q8w).
+  uint8_t* ys8 = nullptr;
+  const uint8_t* xs8 = nullptr;
 };
 
 template <typename T>

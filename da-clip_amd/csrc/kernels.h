@@ -78,6 +78,14 @@ struct ConvArgs {
   int dbuf;
   int gna_nb;
   float gna_eps;
+  // fp8 (OCP e4m3) activations with one E8M0 exponent per (pixel, 32-channel half): the fp8
+  // handles' ResBlock-internal tensor h between block1 and block2 (module_util.py:143-153),
+  // written by block1's epilogue and read only by block2's conv (conv3q.hip).
+  //   ys8 != null: the epilogue writes y as e4m3 bytes (ldy in bytes) and the exponents of pixel
+  //   m to ys8[m * (Cout / 32) + n / 32] (value = e4m3 * 2^(ys8 - 127)).
+  //   xs8: the exponents of an e4m3 input x1 (ld1 in bytes), same layout.
+  uint8_t* ys8;
+  const uint8_t* xs8;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
@@ -132,6 +140,17 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 bool conv8_ok(const ConvArgs& a, int kh, int kw, int s, int p);
 void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, const uint8_t* ws8, int Kp,
            hipStream_t st);
+// fp8 ResBlock pair (conv3q.hip). Producer: a 3x3 conv with ys8 set (block1, 16-bit input) whose
+// epilogue writes e4m3 + exponents; conv_q8out_ok says the dispatcher has such a kernel for it
+// (the weight-stationary 64 -> 64 conv, or the fused-res_conv v4 tiles with Cout = 64).
+// Consumer: block2's 3x3 conv 64 -> 64 over that e4m3 input (x1, xs8, ld1 = 64 bytes) with
+// weight-stationary e4m3 weights q8w [64 out][9 taps][64 in] and exponents q8s [64][9][2]
+// (per output channel, tap and 32-channel half), on the block-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4; 16-bit output with the conv3w epilogue (bias, SiLU, res1).
+bool conv_q8out_ok(const ConvArgs& a);
+bool conv3q_ok(const ConvArgs& a);
+template <typename T>
+void conv3q(const ConvArgs& a, const uint8_t* q8w, const uint8_t* q8s, hipStream_t st);
 
 // Row LayerNorm over C (channel LN of NHWC == token LN):
 //   y = [res +] (x - mean) * rsqrt(var + eps) * g [+ b]

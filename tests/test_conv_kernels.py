@@ -62,3 +62,21 @@ def test_prenorm_layernorm_groupnorm_stats():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
     assert len(rows) == 4 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+
+
+@pytest.mark.gpu
+def test_fp8_resblock_pair_matches_host_reference():
+    """fp8 handles' ResBlock pair (conv3q.hip; module_util.py:143-153): block1's epilogue writes
+    h as e4m3 with one E8M0 exponent per (pixel, 32 channels) — on the 64 -> 64 weight-stationary
+    conv and on the fused-res_conv v4 tiles (64 | 64 concat input, whose 16-bit res_conv output
+    must equal the 16-bit run's bit for bit) — and block2 runs on the block-scaled MFMA over it.
+    Producer: every dequantized value within the e4m3 rounding of the 16-bit output (2^-4
+    relative + 2^(e-8) absolute) and every exponent the smallest (+-1) with max / 2^e <= 448.
+    Consumer: against a host fp64 conv of the dequantized operands with the same epilogue
+    (bias, SiLU, + residual), max-rel < 1e-2 (bf16 output). Timing lines are printed."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "q8", "5"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l for l in out.stdout.splitlines() if "check" in l]
+    assert len(rows) == 2 and all(l.rstrip().endswith("OK") for l in rows), out.stdout

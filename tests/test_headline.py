@@ -114,9 +114,10 @@ def test_headline_bf16_matches_reference(headline, unet_sd):
 
 
 def test_headline_fp8_psnr(headline, unet_sd):
-    """fp8 handles (e4m3 MX GEMMs, BASELINE configs[4]) on the same fixture: the PSNR delta is
-    measured and bounded (measured: dPSNR 7.1e-4 dB, 30.7 dB against the reference's uint8
-    output, float max-rel 4.2e-3); the run must stay finite and batch-invariant."""
+    """fp8 handles (BASELINE configs[4]: e4m3 ResBlock block2 convs + ViT GEMMs) on the same
+    fixture: the PSNR delta is measured and bounded at 2x (measured: dPSNR 1.2e-3 dB, 41.6 dB
+    against the reference's uint8 output, float max-rel 1.5e-3); the run must stay finite and
+    batch-invariant."""
     from daclip_amd.preprocess import tensor2img, calculate_psnr
     g, lq, n0, steps = headline
     ic, dc, out = restore("fp8", g, lq, n0, steps, unet_sd)
@@ -128,5 +129,5 @@ def test_headline_fp8_psnr(headline, unet_sd):
     record("headline_fp8", delta_psnr_db=d_psnr, psnr_vs_ref_u8=calculate_psnr(u8, g["out_u8"]),
            out_rel=rel(out[0], g["out"][0]), ctx_rel=max(rel(ic[0], g["image_context"][0]),
                                                           rel(dc[0], g["degra_context"][0])))
-    assert abs(d_psnr) < 1e-2
-    assert rel(out[0], g["out"][0]) < 2e-2
+    assert abs(d_psnr) < 2.5e-3
+    assert rel(out[0], g["out"][0]) < 3e-3

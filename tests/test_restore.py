@@ -102,17 +102,19 @@ def test_restore_matches_reference(restore_fixture, dtype):
 
 
 def test_restore_fp8_measured(restore_fixture):
-    """fp8 handles (e4m3 MX GEMMs, BASELINE configs[4]): dPSNR measured and bounded (measured
-    -2.31 dB, in-range max-abs 0.156: e4m3's 3-bit significand against a restoration residual
-    that is a small difference of large deep features)."""
+    """fp8 handles (BASELINE configs[4]): the 16-bit (bf16) kernels with the 64 -> 64 ResBlock
+    block2 convs on e4m3 MX operands (block1 writes h as e4m3 + per-(pixel, 32-channel)
+    exponents, conv3q.hip) and the ViT GEMMs on e4m3 MX weights (conv8.hip). dPSNR measured and
+    bounded at 2x the measurement: +0.059 dB, 51.9 dB against the reference's uint8, in-range
+    max-abs 0.053 (round 3's all-conv8 UNet: -2.31 dB, max-abs 0.156)."""
     g, sd, noise = restore_fixture
     _, _, out = restore("fp8", g, sd, noise, 2)
     assert np.array_equal(out[1], out[0])
     assert np.isfinite(out).all()
     m = metrics(g, out[0])
     record("restore_fp8", **m)
-    assert abs(m["delta_psnr_db"]) < 4.0
-    assert m["inrange_max_abs"] < 0.3
+    assert abs(m["delta_psnr_db"]) < 0.12
+    assert m["inrange_max_abs"] < 0.11
 
 
 def test_last_step_from_reference_state(restore_fixture):

@@ -495,8 +495,205 @@ static int gns_check() {
   return fails;
 }
 
+// ---- fp8 ResBlock pair (conv3q.hip): block1 with an e4m3 output (v5 64 -> 64, or the fused
+// res_conv v4 tiles on a 64 | 64 concat), then block2 on the e4m3 tensor.
+//  producer: the dequantized e4m3 output against the same conv's 16-bit output (e4m3 rounding:
+//    |d - y| <= 2^-4 |y| + 2^(e - 9) per value, e the block exponent, plus the 16-bit rounding),
+//    every block exponent the smallest (+-1 at a rounding boundary) with max / 2^e <= 448, and
+//    the fused res_conv output identical to the 16-bit run's;
+//  consumer: against a host fp64 conv of the dequantized input and weights with the same
+//    epilogue (bias, SiLU, + res1), max-rel < 1e-2 (bf16 output rounding);
+//  then times the pair against the 16-bit pair at B = 8, 256^2 (the bench level) and 128^2.
+static void q8_weights(const std::vector<float>& w, std::vector<uint8_t>& w8, std::vector<uint8_t>& s8,
+                       std::vector<float>& deq) {
+  // w: [64][3][3][64] -> e4m3 [64][9][64] + E8M0 [64][9][2] (engine.cpp Packer::make_q8c3)
+  w8.assign(64 * 576, 0); s8.assign(64 * 18, 127); deq.assign(64 * 576, 0.f);
+  for (int n = 0; n < 64; ++n)
+    for (int t = 0; t < 9; ++t)
+      for (int h = 0; h < 2; ++h) {
+        const size_t o = (size_t)n * 576 + t * 64 + 32 * h;
+        float mx = 0.f;
+        for (int c = 0; c < 32; ++c) mx = std::max(mx, std::fabs(w[o + c]));
+        int e = mx > 0.f ? (int)std::ceil(std::log2((double)mx / 448.0)) : 0;
+        e = std::min(126, std::max(-126, e));
+        s8[(size_t)n * 18 + t * 2 + h] = (uint8_t)(127 + e);
+        for (int c = 0; c < 32; ++c) {
+          w8[o + c] = f2e4m3(std::ldexp(w[o + c], -e));
+          deq[o + c] = std::ldexp(e4m3f(w8[o + c]), e);
+        }
+      }
+}
+static int q8_check(int iters) {
+  int fails = 0;
+  struct Q { const char* name; int B, H, W, cin1; bool check; };
+  const Q shapes[] = {{"q8 check 64->64 16x128", 2, 16, 128, 64, true},
+                      {"q8 check 64|64->64 +1x1 8x256", 1, 8, 256, 128, true},
+                      {"q8 256x256 B8 64->64", 8, 256, 256, 64, false},
+                      {"q8 256x256 B8 64|64->64 +1x1", 8, 256, 256, 128, false},
+                      {"q8 128x128 B8 64->64", 8, 128, 128, 64, false}};
+  for (const Q& sh : shapes) {
+    const int B = sh.B, H = sh.H, W = sh.W, C1 = sh.cin1, M = B * H * W;
+    const bool res_in = C1 == 128;
+    uint32_t hs = 777 + C1 + W;
+    auto rnd = [&]() { hs = hs * 1664525u + 1013904223u; return ((hs >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb((size_t)M * C1), rb((size_t)M * 64), w1b((size_t)64 * 9 * C1), w2rb((size_t)64 * C1);
+    for (size_t i = 0; i < xb.size(); ++i) xb[i] = (bf16)(2.f * rnd() * (1 + (i / C1) % 5));
+    for (auto& v : rb) v = (bf16)rnd();
+    for (auto& v : w1b) v = (bf16)(0.1f * rnd());
+    for (auto& v : w2rb) v = (bf16)(0.1f * rnd());
+    std::vector<float> ss((size_t)B * 128), bias2(64), w2f((size_t)64 * 576);
+    for (auto& v : ss) v = 0.5f * rnd();
+    for (auto& v : bias2) v = 0.2f * rnd();
+    for (auto& v : w2f) v = 0.08f * rnd();
+    std::vector<uint8_t> q8w, q8s;
+    std::vector<float> w2d;
+    q8_weights(w2f, q8w, q8s, w2d);
+    std::vector<bf16> w2b(w2f.size());
+    for (size_t i = 0; i < w2f.size(); ++i) w2b[i] = (bf16)w2f[i];
+    void *dx, *dr, *dw1, *dw2r, *dh16, *dy2a, *dy2b, *dz, *dout, *dout16, *dw2b;
+    float *dss, *db2; uint8_t *dh8, *dhs, *dq8w, *dq8s;
+    CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dr, rb.size() * 2)); CK(hipMalloc(&dw1, w1b.size() * 2));
+    CK(hipMalloc(&dw2r, w2rb.size() * 2)); CK(hipMalloc(&dh16, (size_t)M * 128)); CK(hipMalloc(&dy2a, (size_t)M * 128));
+    CK(hipMalloc(&dy2b, (size_t)M * 128)); CK(hipMalloc(&dz, 256)); CK(hipMalloc(&dout, (size_t)M * 128));
+    CK(hipMalloc(&dout16, (size_t)M * 128)); CK(hipMalloc(&dw2b, w2b.size() * 2));
+    CK(hipMalloc(&dss, ss.size() * 4)); CK(hipMalloc(&db2, 256)); CK(hipMalloc(&dh8, (size_t)M * 64));
+    CK(hipMalloc(&dhs, (size_t)M * 2)); CK(hipMalloc(&dq8w, q8w.size())); CK(hipMalloc(&dq8s, q8s.size()));
+    CK(hipMemset(dz, 0, 256));
+    CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dr, rb.data(), rb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw1, w1b.data(), w1b.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw2r, w2rb.data(), w2rb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw2b, w2b.data(), w2b.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dss, ss.data(), ss.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db2, bias2.data(), 256, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dq8w, q8w.data(), q8w.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dq8s, q8s.data(), q8s.size(), hipMemcpyHostToDevice));
+    // block1: x (64, or 64 | 64 as x1 | x2) -> h, scale/shift + SiLU (+ the fused 1x1 res_conv)
+    ConvArgs a1{};
+    a1.x1 = dx; a1.ld1 = C1; a1.C1 = C1; a1.Cin = C1;
+    if (res_in) { a1.x2 = (const bf16*)dx + 64; a1.ld2 = C1; a1.C1 = 64; }
+    a1.Hs = H; a1.Ws = W; a1.B = B; a1.Ho = H; a1.Wo = W; a1.Cout = 64; a1.K = 9 * C1; a1.w = dw1;
+    a1.ss = dss; a1.ss_ld = 128; a1.act = 1; a1.zero = dz; a1.y = dh16; a1.ldy = 64;
+    if (res_in) { a1.w2 = dw2r; a1.y2 = dy2a; a1.ldy2 = 64; }
+    ConvArgs a1q = a1;
+    a1q.y = dh8; a1q.ys8 = dhs;
+    if (res_in) a1q.y2 = dy2b;
+    if (!conv_q8out_ok(a1q)) { printf("%-32s producer not eligible\n", sh.name); ++fails; continue; }
+    // block2: h -> out, SiLU, + res (the 16-bit pair reads h16 with the bf16-rounded weights)
+    ConvArgs a2{};
+    a2.x1 = dh16; a2.ld1 = 64; a2.C1 = 64; a2.Cin = 64; a2.Hs = H; a2.Ws = W; a2.B = B; a2.Ho = H; a2.Wo = W;
+    a2.Cout = 64; a2.K = 576; a2.w = dw2b; a2.bias = db2; a2.act = 1; a2.zero = dz; a2.res1 = dr; a2.ldr1 = 64;
+    a2.y = dout16; a2.ldy = 64;
+    ConvArgs a2q = a2;
+    a2q.x1 = dh8; a2q.xs8 = dhs; a2q.y = dout; a2q.w = nullptr;
+    if (!conv3q_ok(a2q)) { printf("%-32s consumer not eligible\n", sh.name); ++fails; continue; }
+    conv<bf16>(a1, 3, 3, 1, 1, 0);
+    conv<bf16>(a1q, 3, 3, 1, 1, 0);
+    conv3q<bf16>(a2q, dq8w, dq8s, 0);
+    conv<bf16>(a2, 3, 3, 1, 1, 0);
+    CK(hipDeviceSynchronize());
+    if (sh.check) {
+      std::vector<bf16> h16((size_t)M * 64), y2a, y2b, o((size_t)M * 64);
+      std::vector<uint8_t> h8((size_t)M * 64), e8((size_t)M * 2);
+      CK(hipMemcpy(h16.data(), dh16, h16.size() * 2, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h8.data(), dh8, h8.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(e8.data(), dhs, e8.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(o.data(), dout, o.size() * 2, hipMemcpyDeviceToHost));
+      int bad_v = 0, bad_e = 0;
+      std::vector<float> hd((size_t)M * 64);
+      for (int m = 0; m < M; ++m)
+        for (int hf = 0; hf < 2; ++hf) {
+          const int e = (int)e8[(size_t)m * 2 + hf] - 127;
+          float mx = 0.f, mq = 0.f;
+          for (int c = 32 * hf; c < 32 * hf + 32; ++c) {
+            const size_t i = (size_t)m * 64 + c;
+            const float y = bf2f(h16[i]), d = std::ldexp(e4m3f(h8[i]), e);
+            hd[i] = d;
+            mx = std::max(mx, std::fabs(y));
+            mq = std::max(mq, std::fabs(e4m3f(h8[i])));
+            if (!(std::fabs(d - y) <= 0.0703f * std::fabs(y) + std::ldexp(1.f, e - 8))) {
+              if (bad_v < 4) printf("   h m=%d c=%d got %g want %g (e %d)\n", m, c, d, y, e);
+              ++bad_v;
+            }
+          }
+          const int eh = mx > 0.f ? (int)std::ceil(std::log2(mx / 440.0)) : -126;
+          if (mq > 448.f || std::abs(e - std::max(-126, eh)) > 1) {
+            if (bad_e < 4) printf("   exponent m=%d half %d: %d (host %d, max code %g)\n", m, hf, e, eh, mq);
+            ++bad_e;
+          }
+        }
+      if (res_in) {
+        y2a.resize((size_t)M * 64); y2b.resize((size_t)M * 64);
+        CK(hipMemcpy(y2a.data(), dy2a, (size_t)M * 128, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(y2b.data(), dy2b, (size_t)M * 128, hipMemcpyDeviceToHost));
+        if (memcmp(y2a.data(), y2b.data(), (size_t)M * 128)) { printf("   fused res_conv output differs\n"); ++bad_v; }
+      }
+      double md = 0, mref = 0;
+      int shown = 0;
+      for (int b = 0; b < B; ++b)
+        for (int oh = 0; oh < H; ++oh)
+          for (int ow = 0; ow < W; ++ow)
+            for (int n = 0; n < 64; ++n) {
+              double acc = 0;
+              for (int kh = 0; kh < 3; ++kh)
+                for (int kw = 0; kw < 3; ++kw) {
+                  const int ih = oh + kh - 1, iw = ow + kw - 1;
+                  if (ih < 0 || iw < 0 || ih >= H || iw >= W) continue;
+                  const float* xp = &hd[(((size_t)b * H + ih) * W + iw) * 64];
+                  const float* wp = &w2d[(size_t)n * 576 + (kh * 3 + kw) * 64];
+                  for (int c = 0; c < 64; ++c) acc += (double)xp[c] * wp[c];
+                }
+              acc += bias2[n];
+              acc = acc / (1.0 + std::exp(-acc));
+              const size_t i = (((size_t)b * H + oh) * W + ow) * 64 + n;
+              acc += bf2f(rb[i]);
+              const double g = bf2f(o[i]);
+              if (shown < 4 && !(std::fabs(g - acc) <= 1e-2 * std::max(1.0, std::fabs(acc)))) {
+                printf("   out b=%d oh=%d ow=%d n=%d got %g want %g\n", b, oh, ow, n, g, acc);
+                ++shown;
+              }
+              md = std::max(md, std::fabs(g - acc));
+              mref = std::max(mref, std::fabs(acc));
+            }
+      const bool ok = bad_v == 0 && bad_e == 0 && md / mref < 1e-2;
+      printf("%-32s producer: %d bad values, %d bad exponents; consumer rel %.2e  check %s\n", sh.name, bad_v, bad_e,
+             md / mref, ok ? "OK" : "FAIL");
+      fails += !ok;
+    } else {
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+      auto tm = [&](auto fn) {
+        for (int i = 0; i < 3; ++i) fn();
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; ++i) fn();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        return ms * 1e3 / iters;
+      };
+      double t1 = tm([&] { conv<bf16>(a1, 3, 3, 1, 1, 0); });
+      double t1q = tm([&] { conv<bf16>(a1q, 3, 3, 1, 1, 0); });
+      // (second, interleaved pass: the chip's clock drifts between the first launches)
+      t1 = std::min(t1, tm([&] { conv<bf16>(a1, 3, 3, 1, 1, 0); }));
+      t1q = std::min(t1q, tm([&] { conv<bf16>(a1q, 3, 3, 1, 1, 0); }));
+      const double t2 = tm([&] { conv<bf16>(a2, 3, 3, 1, 1, 0); });
+      const double t2q = tm([&] { conv3q<bf16>(a2q, dq8w, dq8s, 0); });
+      const double fl2 = 2.0 * M * 64 * 576;
+      printf("%-32s block1 16-bit %6.1f us, e4m3 out %6.1f us | block2 16-bit %6.1f us (%5.0f TF/s), e4m3 %6.1f us "
+             "(%5.0f TF/s) | pair %6.1f -> %6.1f us\n", sh.name, t1, t1q, t2, fl2 / t2 / 1e6, t2q, fl2 / t2q / 1e6,
+             t1 + t2, t1q + t2q);
+      CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
+    }
+    for (void* p : {dx, dr, dw1, dw2r, dh16, dy2a, dy2b, dz, dout, dout16, dw2b}) CK(hipFree(p));
+    for (void* p : {(void*)dss, (void*)db2, (void*)dh8, (void*)dhs, (void*)dq8w, (void*)dq8s}) CK(hipFree(p));
+  }
+  return fails;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
+  if (argc > 1 && !strcmp(argv[1], "q8")) return q8_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "gns")) return gns_check();
   if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
   int iters = argc > 1 ? atoi(argv[1]) : 20;

@@ -8,7 +8,7 @@ TAG=${1:-r}
 O=gpurun_out/round_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-PMC_DTYPES="bf16 fp32" bash tools/pmc_bench.sh $TAG || { echo PMC FAILED; exit 1; }
+PMC_DTYPES="${PMC_DTYPES:-fp16 fp32}" bash tools/pmc_bench.sh $TAG || { echo PMC FAILED; exit 1; }
 python3 tools/pmc_traffic.py gpurun_out/pmc_$TAG profiles/pmc_traffic.json > $O/pmc_traffic.txt || exit 1
 cp profiles/pmc_traffic.json $O/pmc_traffic.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { echo TESTS FAILED; tail -30 $O/tests.log; exit 1; }
