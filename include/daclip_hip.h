@@ -45,9 +45,11 @@ extern "C" {
 
 typedef struct dac_handle dac_handle;
 
-/* compute/storage dtype. DAC_FP8: bf16 activations, and every conv / linear whose input
- * channels are a multiple of 64 runs on the block-scaled fp8 MFMA (OCP e4m3 weights and
- * on-the-fly quantized activations, one E8M0 scale per 64-element block; BASELINE configs[4]).
+/* compute/storage dtype. DAC_FP8 (BASELINE configs[4]): bf16 activations and kernels, with
+ * the block-scaled fp8 MFMA where its operands arrive as OCP e4m3 without VALU work: the UNet's
+ * 64 -> 64 ResBlock block2 convs read the e4m3 tensor (one E8M0 exponent per pixel and 32
+ * channels) that block1's epilogue writes, with e4m3 weights (one exponent per output channel,
+ * tap and 32 input channels); the ViT's GEMMs take e4m3 weights (one exponent per 64 k).
  * DAC_F16: IEEE half weights and activations on the f16 MFMA, fp32 accumulate — the same
  * bytes and MFMA rate as DAC_BF16 with an 11-bit instead of 8-bit significand. */
 enum dac_dtype { DAC_F32 = 0, DAC_BF16 = 1, DAC_FP8 = 2, DAC_F16 = 3 };
