@@ -26,7 +26,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // (narrow Cout), 15 / 16 / 17 / 18 = v2 1x1 128x256 (GEGLU) / 256x256 / 64x128 / 128x64,
 // 2-stage, 20 = v4 with 32-pixel wave tiles 128x64, 21 = v5 weight-stationary 3x3 (64 -> 64),
 // 22 / 23 = conv_edge.hip init_conv (7x7, Cin 8, Cout 64) / final_conv (3x3, Cout <= 4),
-// 24 = conv_down.hip (4x4 stride-2 Downsample), 25 = v6 2-D halo 3x3 (conv3h_kernel).
+// 24 = conv_down.hip (4x4 stride-2 Downsample), 25 = v6 2-D halo 3x3 (conv3h_kernel), 26 = v4
+// row-phase upsample conv (ConvArgs::uph; labelled by the engine, not returned here).
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -124,7 +125,7 @@ bool conv_gna_ok(const ConvArgs& a, int elem_bytes) {
 // row pitch, 31-bit byte offsets), the minimal register epilogue, no fused second output.
 bool conv3h_ok(const ConvArgs& a, int elem_bytes) {
   if (elem_bytes != 2 || !a.zero || a.amode != 0 || a.cwrap != 0 || a.w_bstride != 0 || a.y2 || a.ln_g || a.lnf_cs ||
-      a.gna_stats || a.ys8 || a.xs8)
+      a.gna_stats || a.ys8 || a.xs8 || a.uph)
     return false;
   if (a.Cin % 32 || (a.C1 < a.Cin && a.C1 % 32) || a.K != 9 * a.Cin || a.Cout % 64 || a.Wo % 64 || a.Ho % 8)
     return false;
@@ -160,6 +161,21 @@ bool conv_q8out_ok(const ConvArgs& a0) {
     return conv3w_ok(a) && buf;
   }
   return conv_res_fusable(a) && conv_variant(a, 3, 2) == 12;
+}
+
+// Row-phase upsample conv (ConvArgs::uph; the caller passes the 4-row phase weights with
+// K = 12 Cin): mirrors the dispatcher's uph branch — 16-bit v4 256x64 swapped tiles whose RH
+// output rows fit a whole number of row pairs, minimal epilogue, no second output.
+bool conv_uph_ok(const ConvArgs& a) {
+  if (!a.up || !a.zero || a.amode || a.cwrap || a.w_bstride || a.y2 || a.ys8 || a.xs8 || a.ln_g || a.lnf_cs ||
+      a.gna_stats || g_conv3_force >= 0)
+    return false;
+  if (a.Cout % 64 || a.Cin % 64 || (a.C1 < a.Cin && a.C1 % 32) || a.K != 12 * a.Cin) return false;
+  if (!(a.act == ACT_NONE || a.act == ACT_SILU) || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8))
+    return false;
+  if ((a.ss && (a.ss_ld % 4 || a.Cout % 4 || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
+  const int RW = conv3_rw_host(a, 256);
+  return RW > 0 && RW % 64 == 0 && a.Ho % (2 * (256 / RW)) == 0;
 }
 
 template <typename T>

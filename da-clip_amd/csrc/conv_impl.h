@@ -1051,7 +1051,14 @@ conv3i_kernel(ConvArgs a, int RW) {
   const int tiles_img = (a.Ho / RH) * tiles_w;
   const int b = tl.bx / tiles_img;
   const int tr = tl.bx - b * tiles_img;
-  const int oh0 = (tr / tiles_w) * RH, ow0 = (tr % tiles_w) << rws;
+  // FL bit 13 (row-phase upsample conv, ConvArgs::uph): tile row index tri = 2g + a holds the
+  // output rows 2 RH g + a + 2y (one parity a), stride 2 Wo; its kernel-row stages s2 = 0, 1 read
+  // source rows as kernel rows kh = s2 + a of the plain conv and weight rows 2a + s2.
+  constexpr bool UPH = (FL & 8192) != 0;
+  const int tri = tr / tiles_w;
+  const int ph = UPH ? (tri & 1) : 0;
+  const int oh0 = UPH ? 2 * RH * (tri >> 1) + ph : tri * RH, ow0 = (tr % tiles_w) << rws;
+  constexpr int KHN = UPH ? 2 : 3;                         // kernel-row stages per chunk
   const int n0 = tl.by * BN;
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   const char* zero = reinterpret_cast<const char*>(a.zero);
@@ -1065,7 +1072,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   constexpr bool BUF = (FL & 1024) != 0;
   constexpr unsigned OOB = 0x80000000u;
   // A DMA: instruction j of this wave fills physical rows (wave + j*NW)*RPI + lane/SLOTS.
-  int a_pix[AGX][3], a_ls[AGX];
+  int a_pix[AGX][KHN], a_ls[AGX];
 #pragma unroll
   for (int j = 0; j < AGX; ++j) {
     const int P = (wave + j * NW) * RPI + lane / SLOTS;
@@ -1073,8 +1080,8 @@ conv3i_kernel(ConvArgs a, int RW) {
     a_ls[j] = SA::slot(R, lane % SLOTS) * VE;
     const int oy = R / RWP, iw = ow0 + (R - oy * RWP) - 1;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
-      const int ih = oh0 + oy + kh - 1;
+    for (int kh = 0; kh < KHN; ++kh) {
+      const int ih = UPH ? oh0 + 2 * oy + kh + ph - 1 : oh0 + oy + kh - 1;
       int pix = -1;
       if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
         pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
@@ -1156,7 +1163,7 @@ conv3i_kernel(ConvArgs a, int RW) {
       for (int j = 0; j < AGX; ++j)
         if (wave + j * NW < NA)                                  // wave-uniform
           buf_lds16(from1 ? a.x1 : a.x2, x_bytes, st + (wave + j * NW) * RPI * CK, a_pix[j][kh], soa);
-      const int sob = (kh * 3 * a.Cin + ci0) * ES;
+      const int sob = ((UPH ? 2 * ph + kh : kh) * 3 * a.Cin + ci0) * ES;
 #pragma unroll
       for (int j = 0; j < BGX; ++j)
         if (BGX == BGN || wave + j * NW < NB)                    // wave-uniform
@@ -1184,7 +1191,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
     for (int j = 0; j < BGX; ++j) {
       if (BGX == BGN || wave + j * NW < NB) {                   // wave-uniform
-        const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + kh * 3 * a.Cin + ci0 + b_ls[j])
+        const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + (UPH ? 2 * ph + kh : kh) * 3 * a.Cin + ci0 + b_ls[j])
                                    : zero;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                          (lds_void_t*)(st + AROWS * CK + (wave + j * NW) * RPI * CK),
@@ -1279,7 +1286,8 @@ conv3i_kernel(ConvArgs a, int RW) {
 
   // Stage s = 3*c + kh. The loop is unrolled over kh so every issue() has a static kh: the
   // stage issued at (c, kh) is s + ST - 1 = (c + (kh + ST - 1) / 3, (kh + ST - 1) % 3).
-  const int nchunk = a.Cin / BKE, S = 3 * nchunk;
+  static_assert(!UPH || (ST == 2 && !RES), "row-phase tiles: 2 stages, no fused res_conv");
+  const int nchunk = a.Cin / BKE, S = KHN * nchunk;
   issue(0, std::integral_constant<int, 0>{}, 0);
   if constexpr (SWAP) {
     if (wave == 0) {                              // lanes 0-15 scale, 16-31 shift, 32-47 bias
@@ -1300,21 +1308,22 @@ conv3i_kernel(ConvArgs a, int RW) {
   const bool pre_ok = SWAP && !RES && a.res1 && !a.res2 && !a.bbias && !a.ss;
   EpiPref<TM> pref;
   const int rm_base = b * HWo + oh0 * a.Wo + ow0;
+  const int rstride = UPH ? 2 * a.Wo : a.Wo;              // output row stride of the tile
   auto pixf = [&](int i) {
     const int t = wm * WTM + TM * lr + i;
-    return (size_t)(rm_base + (t >> rws) * a.Wo + (t & ((1 << rws) - 1)));
+    return (size_t)(rm_base + (t >> rws) * rstride + (t & ((1 << rws) - 1)));
   };
   auto step = [&](int c, auto khc) {
     constexpr int kh = decltype(khc)::value;
-    constexpr int KN = (kh + ST - 1) % 3, CN = (kh + ST - 1) / 3;
-    const int s = 3 * c + kh;
+    constexpr int KN = (kh + ST - 1) % KHN, CN = (kh + ST - 1) / KHN;
+    const int s = KHN * c + kh;
     if constexpr (FL & 1) __builtin_amdgcn_sched_barrier(0);
     if (s + ST - 2 < S) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VMW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     if constexpr ((FL & 256) == 0) __builtin_amdgcn_s_barrier();   // (FL 256: diagnostic, no barrier)
     asm volatile("" ::: "memory");
     if (s + ST - 1 < S) issue(c + CN, std::integral_constant<int, KN>{}, nbuf);
-    if constexpr (SWAP && kh == 2) {
+    if constexpr (SWAP && kh == KHN - 1) {
       if (s + 1 == S && pre_ok) {
         const int nb = n0 + wn * WTN + 16 * lg;
         epi_prefetch<T, TM>(a, nb, b, pixf, pref);
@@ -1328,14 +1337,14 @@ conv3i_kernel(ConvArgs a, int RW) {
   for (int c = 0; c < nchunk; ++c) {
     step(c, std::integral_constant<int, 0>{});
     step(c, std::integral_constant<int, 1>{});
-    step(c, std::integral_constant<int, 2>{});
+    if constexpr (!UPH) step(c, std::integral_constant<int, 2>{});
   }
   struct Rows {
     int base, rws, Wo;
     DEV int operator()(int t) const { return base + (t >> rws) * Wo + (t & ((1 << rws) - 1)); }
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
+  const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, rstride};
   if constexpr ((FL & 128) != 0) {                 // diagnostic: no epilogue (all MFMA chains kept live)
     float t = 0.f;
 #pragma unroll
@@ -1397,6 +1406,11 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
   }
   if constexpr ((FL & 16) != 0)   // fused res_conv: writes y2 from w2, so both must be given
     if (!a.y2 || !a.w2) return false;
+  if constexpr ((FL & 8192) != 0) {   // row-phase upsample tiles: one parity per tile
+    if (!a.up || !a.uph || a.Ho % (2 * (BM / RW))) return false;
+  } else if (a.uph) {
+    return false;
+  }
   if constexpr ((FL & 8) != 0)    // swapped tiles DMA the scale / shift / bias rows in 16-byte pieces
     if ((a.ss && (a.ss_ld % 4 || (a.Cout % 4) || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   dim3 g(a.B * a.Ho * a.Wo / BM, (a.Cout + BN - 1) / BN, 1);
@@ -2064,6 +2078,11 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         if constexpr (sizeof(T) == 2) {
           // Buffer-resource DMA (FL bit 10) first; the flat-address form takes what it rejects.
           const int nb = g_conv3_buf ? 1024 : 0;
+          if (a.uph) {                                // row-phase upsample conv (conv_uph_ok)
+            if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 8192>(a, st)) return;
+            if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192>(a, st)) return;
+            abort();
+          }
           if (a.ys8) {                                // fp8 output (conv_q8out_ok): fused-res tiles only
             if (a.y2 && a.Cout == 64 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024 | 4096>(a, st)) return;
             if (a.y2 && a.Cout == 64 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 4096>(a, st)) return;

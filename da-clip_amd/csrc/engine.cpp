@@ -254,6 +254,27 @@ struct Packer {
   bool q8 = false;                     // fp8 handles' UNet: e4m3 64 -> 64 ResBlock block2 weights
   static constexpr int VE = sizeof(T) == 2 ? 8 : 4;
 
+  // Row-phase weights of a 3x3 conv applied after a 2x nearest upsample (ConvArgs::uph): output
+  // row 2i reads source rows (i-1 | i, i) and row 2i+1 (i, i | i+1), so the kernel rows fold to
+  // (W0, W1+W2) and (W0+W1, W2), summed in fp32 and rounded to T once.
+  void make_uph(ConvW& cw, const std::vector<float>& p, const std::string& key) {
+    if (sizeof(T) != 2 || cw.kh != 3 || cw.kw != 3 || cw.kwp || p.size() != (size_t)cw.cout * 9 * cw.cin) return;
+    if (getenv("DAC_UPH") && atoi(getenv("DAC_UPH")) == 0) return;
+    const size_t R = (size_t)3 * cw.cin;                 // one kernel row [3][cin]
+    std::vector<float> q((size_t)cw.cout * 4 * R);
+    for (int o = 0; o < cw.cout; ++o) {
+      const float* w = &p[(size_t)o * 3 * R];
+      float* d = &q[(size_t)o * 4 * R];
+      for (size_t k = 0; k < R; ++k) {
+        d[k] = w[k];
+        d[R + k] = w[R + k] + w[2 * R + k];
+        d[2 * R + k] = w[k] + w[R + k];
+        d[3 * R + k] = w[2 * R + k];
+      }
+    }
+    cw.wph = upload_T(q, key, 12, cw.cin);
+  }
+
   // conv3q weights of a 3x3 64 -> 64 conv from its packed [64][3][3][64] fp32 values: e4m3 bytes
   // [64][9][64] with one E8M0 exponent per (output channel, tap, 32-channel half), the smallest
   // with max |w| / 2^e <= 448.
@@ -527,6 +548,16 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   ConvArgs a = conv_args(r, cw, x1, ld1, C1, x2, ld2, B, Hs, Ws, up, stride, pad, y, ldy, e);
   const double M = (double)B * a.Ho * a.Wo;
   double fl = 2.0 * M * cw.cout * cw.kh * cw.kw * cw.cin_real;
+  if (cw.wph && up && stride == 1 && pad == 1 && !cw.dual && !e.fuse1x1) {
+    // Row-phase form (ConvArgs::uph): 6 of the 9 taps' work per output pixel.
+    ConvArgs q = a;
+    q.w = cw.wph; q.K = 12 * cw.cin; q.uph = 1;
+    if (!r.zero) q.zero = &q;                        // (dry runs carry no zero page)
+    if (conv_uph_ok(q)) {
+      a.w = cw.wph; a.K = 12 * cw.cin; a.uph = 1;
+      fl = 2.0 * M * cw.cout * 6 * cw.cin_real;
+    }
+  }
   Profiler* p = r.prof;
   const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
   bool fused = false;
@@ -543,7 +574,8 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   }
   r.flops += fl;
   // Class 340: the fp8 ResBlock block2 (conv3q); an fp8-output block1 keeps its kernel's class.
-  const int cls = cw.kh * 100 + (a.xs8 ? 40 : use8 ? 30 : conv_variant(a, cw.kh, (int)sizeof(T)));
+  // Class 326: the row-phase upsample conv on v4 tiles (kept out of class 312's roofline).
+  const int cls = cw.kh * 100 + (a.xs8 ? 40 : use8 ? 30 : a.uph ? 26 : conv_variant(a, cw.kh, (int)sizeof(T)));
   const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == cls);
   if (r.dry) {
     if (timed) p->used++;
@@ -814,7 +846,9 @@ struct UNetNet {
                             : P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", false, kwp7);
     if (half) {
       half_down = P.conv("downsample.weight", nf, nf, 4, 4, "downsample.bias");
-      half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias");
+      std::vector<float> pk;
+      half_up = P.conv("upsample.1.weight", nf, nf, 3, 3, "upsample.1.bias", false, 0, &pk);
+      P.make_uph(half_up, pk, "upsample.1.weight");
     }
     tm1w = P.f32("time_mlp.1.weight", {tdim, nf});
     tm1b = P.f32("time_mlp.1.bias", {tdim});
@@ -848,8 +882,13 @@ struct UNetNet {
       L.b1 = load_rb(P, p + "0.", dout + din, dout);
       L.b2 = load_rb(P, p + "1.", dout + din, dout);
       L.at = load_attn(P, p + "2.", dout, imgctx && i >= st_from);
-      L.samp = i != 0 ? P.conv(p + "3.1.weight", din, dout, 3, 3, p + "3.1.bias")
-                      : P.conv(p + "3.weight", din, dout, 3, 3);
+      if (i != 0) {                                  // Upsample: nearest 2x, then this 3x3
+        std::vector<float> pk;
+        L.samp = P.conv(p + "3.1.weight", din, dout, 3, 3, p + "3.1.bias", false, 0, &pk);
+        P.make_uph(L.samp, pk, p + "3.1.weight");
+      } else {
+        L.samp = P.conv(p + "3.weight", din, dout, 3, 3);
+      }
     }
     const int mid = levels.back().second;
     mid1 = load_rb(P, "mid_block1.", mid, mid);

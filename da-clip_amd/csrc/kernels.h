@@ -86,6 +86,12 @@ struct ConvArgs {
   //   xs8: the exponents of an e4m3 input x1 (ld1 in bytes), same layout.
   uint8_t* ys8;
   const uint8_t* xs8;
+  // Row-phase form of a 3x3 conv over a 2x nearest-upsampled input (up = 1; the UNet's
+  // Upsample, module_util.py:100-103): output row 2i+a reads source rows (i-1, i, i) for a = 0
+  // and (i, i, i+1) for a = 1, so its three kernel rows collapse to two with summed weights.
+  // uph = 1: w is [Cout][4 rows][3][Cin] = (W0, W1+W2 | W0+W1, W2), K = 12 Cin, and the v4 tiles
+  // hold output rows of one parity (2 kernel-row stages per chunk instead of 3).
+  int uph;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
@@ -148,6 +154,8 @@ void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, c
 // (per output channel, tap and 32-channel half), on the block-scaled MFMA
 // v_mfma_scale_f32_16x16x128_f8f6f4; 16-bit output with the conv3w epilogue (bias, SiLU, res1).
 bool conv_q8out_ok(const ConvArgs& a);
+// Row-phase upsample conv (ConvArgs::uph): the dispatcher has the kernel for this conv.
+bool conv_uph_ok(const ConvArgs& a);
 bool conv3q_ok(const ConvArgs& a);
 template <typename T>
 void conv3q(const ConvArgs& a, const uint8_t* q8w, const uint8_t* q8s, hipStream_t st);

@@ -80,3 +80,18 @@ def test_fp8_resblock_pair_matches_host_reference():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
     assert len(rows) == 2 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+
+
+@pytest.mark.gpu
+def test_row_phase_upsample_conv_matches_plain():
+    """The UNet's Upsample convs (nearest 2x then 3x3, module_util.py:100-103) in row-phase form
+    (ConvArgs::uph: output row 2i+a reads source rows (i-1, i, i) or (i, i, i+1), so its kernel
+    rows fold to (W0, W1+W2) / (W0+W1, W2) and each chunk takes 2 stages instead of 3) against
+    the plain up conv with the same fp32 weights at the three UNet shapes: max-rel < 1e-2 (the
+    folded rows round to bf16 once; measured ~5e-3). Timing lines are printed."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "uph", "5"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l for l in out.stdout.splitlines() if "check" in l]
+    assert len(rows) == 3 and all(l.rstrip().endswith("OK") for l in rows), out.stdout

@@ -691,8 +691,87 @@ static int q8_check(int iters) {
   return fails;
 }
 
+// ---- row-phase upsample conv (ConvArgs::uph): the UNet's Upsample convs (nearest 2x, then
+// 3x3) as two kernel rows per output-row parity with summed weights, against the plain up conv
+// with the same fp32 weights (each rounded to bf16: the folded rows round once, so the bound
+// is the bf16 rounding, max-rel < 1e-2), then both timed at B = 8.
+static int uph_check(int iters) {
+  struct U { const char* name; int B, Hs, Ws, cin, cout; };
+  const U shapes[] = {{"uph 128^2->256^2 128->64", 8, 128, 128, 128, 64},
+                      {"uph 64^2->128^2 256->128", 8, 64, 64, 256, 128},
+                      {"uph 32^2->64^2 512->256", 8, 32, 32, 512, 256}};
+  int fails = 0;
+  for (const U& sh : shapes) {
+    const int Ho = 2 * sh.Hs, Wo = 2 * sh.Ws, M = sh.B * Ho * Wo, C = sh.cin, N = sh.cout;
+    uint32_t hs = 4242 + C;
+    auto rnd = [&]() { hs = hs * 1664525u + 1013904223u; return ((hs >> 8) & 0xffff) / 65535.f - 0.5f; };
+    std::vector<bf16> xb((size_t)sh.B * sh.Hs * sh.Ws * C), wb((size_t)N * 9 * C), pb((size_t)N * 12 * C);
+    std::vector<float> wf((size_t)N * 9 * C), bias(N);
+    for (auto& v : xb) v = (bf16)(2.f * rnd());
+    for (auto& v : wf) v = 0.05f * rnd();
+    for (auto& v : bias) v = 0.1f * rnd();
+    for (size_t i = 0; i < wf.size(); ++i) wb[i] = (bf16)wf[i];
+    const size_t R = (size_t)3 * C;
+    for (int o = 0; o < N; ++o)
+      for (size_t k = 0; k < R; ++k) {
+        const float* w = &wf[(size_t)o * 3 * R];
+        bf16* d = &pb[(size_t)o * 4 * R];
+        d[k] = (bf16)w[k]; d[R + k] = (bf16)(w[R + k] + w[2 * R + k]);
+        d[2 * R + k] = (bf16)(w[k] + w[R + k]); d[3 * R + k] = (bf16)w[2 * R + k];
+      }
+    void *dx, *dw, *dp, *dz, *dy0, *dy1; float* db;
+    CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dw, wb.size() * 2)); CK(hipMalloc(&dp, pb.size() * 2));
+    CK(hipMalloc(&dz, 256)); CK(hipMalloc(&dy0, (size_t)M * N * 2)); CK(hipMalloc(&dy1, (size_t)M * N * 2));
+    CK(hipMalloc(&db, N * 4));
+    CK(hipMemset(dz, 0, 256));
+    CK(hipMemcpy(dx, xb.data(), xb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, wb.data(), wb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dp, pb.data(), pb.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, bias.data(), N * 4, hipMemcpyHostToDevice));
+    ConvArgs a{};
+    a.x1 = dx; a.ld1 = C; a.C1 = C; a.Cin = C; a.Hs = sh.Hs; a.Ws = sh.Ws; a.up = 1; a.B = sh.B; a.Ho = Ho;
+    a.Wo = Wo; a.Cout = N; a.K = 9 * C; a.w = dw; a.bias = db; a.zero = dz; a.y = dy0; a.ldy = N;
+    ConvArgs u = a;
+    u.w = dp; u.K = 12 * C; u.uph = 1; u.y = dy1;
+    if (!conv_uph_ok(u)) { printf("%-28s not eligible\n", sh.name); ++fails; continue; }
+    conv<bf16>(a, 3, 3, 1, 1, 0);
+    conv<bf16>(u, 3, 3, 1, 1, 0);
+    CK(hipDeviceSynchronize());
+    std::vector<bf16> y0((size_t)M * N), y1((size_t)M * N);
+    CK(hipMemcpy(y0.data(), dy0, y0.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(y1.data(), dy1, y1.size() * 2, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < y0.size(); ++i) {
+      md = std::max(md, std::fabs((double)bf2f(y1[i]) - bf2f(y0[i])));
+      mx = std::max(mx, std::fabs((double)bf2f(y0[i])));
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    auto tm = [&](const ConvArgs& c) {
+      for (int i = 0; i < 3; ++i) conv<bf16>(c, 3, 3, 1, 1, 0);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) conv<bf16>(c, 3, 3, 1, 1, 0);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      return ms * 1e3 / iters;
+    };
+    double t0 = tm(a), t1 = tm(u);
+    t0 = std::min(t0, tm(a));
+    t1 = std::min(t1, tm(u));
+    const bool ok = md / mx < 1e-2;
+    printf("%-28s plain %6.1f us, row-phase %6.1f us  check rel %.2e %s\n", sh.name, t0, t1, md / mx, ok ? "OK" : "FAIL");
+    fails += !ok;
+    for (void* p : {dx, dw, dp, dz, dy0, dy1, (void*)db}) CK(hipFree(p));
+    CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
+  }
+  return fails;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
+  if (argc > 1 && !strcmp(argv[1], "uph")) return uph_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "q8")) return q8_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "gns")) return gns_check();
   if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
