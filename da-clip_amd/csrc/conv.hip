@@ -170,12 +170,12 @@ bool conv_uph_ok(const ConvArgs& a) {
   if (!a.up || !a.zero || a.amode || a.cwrap || a.w_bstride || a.y2 || a.ys8 || a.xs8 || a.ln_g || a.lnf_cs ||
       a.gna_stats || g_conv3_force >= 0)
     return false;
-  if (a.Cout % 64 || a.Cin % 64 || (a.C1 < a.Cin && a.C1 % 32) || a.K != 12 * a.Cin) return false;
+  if (a.Cout % 64 || a.Cin % 64 || (a.C1 < a.Cin && a.C1 % 32) || a.K != (a.uph == 2 ? 16 : 12) * a.Cin) return false;
   if (!(a.act == ACT_NONE || a.act == ACT_SILU) || a.ldy % 8 || (a.res1 && a.ldr1 % 8) || (a.res2 && a.ldr2 % 8))
     return false;
   if ((a.ss && (a.ss_ld % 4 || a.Cout % 4 || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   const int RW = conv3_rw_host(a, 256);
-  return RW > 0 && RW % 64 == 0 && a.Ho % (2 * (256 / RW)) == 0;
+  return RW > 0 && RW % 64 == 0 && a.Ho % (2 * (256 / RW)) == 0 && (a.uph != 2 || RW >= 128);
 }
 
 template <typename T>

@@ -1010,16 +1010,24 @@ conv3i_kernel(ConvArgs a, int RW) {
   constexpr int AGX = (NA_MAX + NW - 1) / NW;                // A DMA instructions per wave (max)
   constexpr int AGN = NA_MIN / NW;                           // ... (min, for the vmcnt count)
   constexpr int AROWS = NA_MAX * RPI;
-  constexpr int NB = 3 * BN / RPI;                           // B DMA instructions per stage
+  // FL bit 14 (with 13): column-phase too — the waves of a tile each hold output columns of one
+  // parity b, whose three kernel columns fold to two taps over the SOURCE columns like the rows:
+  // (W.0, W.1+W.2 | W.0+W.1, W.2). The halo is then source pixels (RW/2 + 2 per row, no
+  // duplicates) and a stage's weight rows are the 4 (b, tap) sets: w is [Cout][4 row sets][4][Cin].
+  constexpr bool UPC = (FL & 16384) != 0;
+  constexpr int NBR = UPC ? 4 : 3;                           // weight-row sets per stage
+  constexpr int NTAP = UPC ? 2 : 3;                          // taps per wave per stage
+  constexpr int NB = NBR * BN / RPI;                         // B DMA instructions per stage
   constexpr int BGX = (NB + NW - 1) / NW, BGN = NB / NW;     // per wave (max / min)
   // FL bit 4: fused 1x1 second output (ConvArgs::w2 / y2): the centre-tap A fragments of the
   // kh = 1 stages also multiply the w2 rows (hi and lo parts), staged after the 3*BN weight
   // rows, into a second accumulator set written by a plain register epilogue.
   constexpr bool RES = (FL & 16) != 0;
   constexpr int RROWS = RES ? 2 * BN : 0;
-  constexpr int STAGE = (AROWS + 3 * BN + RROWS) * CK;
+  constexpr int STAGE = (AROWS + NBR * BN + RROWS) * CK;
   static_assert(SLOTS == 8 || SLOTS == 4, "CK");
-  static_assert((3 * BN) % RPI == 0 && KSTEPS >= 1 && TM >= 1 && TN >= 1, "tile");
+  static_assert((NBR * BN) % RPI == 0 && KSTEPS >= 1 && TM >= 1 && TN >= 1, "tile");
+  static_assert(!UPC || ((FL & 8192) && (FL & 8) && !RES && WGN == 1 && WTM == 64), "column-phase tiles");
   static_assert(!RES || (ST == 2 && (FL & 8) && BN % RPI == 0), "fused res: swapped tiles, 2 stages");
   static_assert(STAGE % 256 == 0 && (AROWS * CK) % 256 == 0, "bank-line aligned regions");
   static_assert(ST == 2 || ST == 3 || ST == 4, "stages");
@@ -1044,7 +1052,7 @@ conv3i_kernel(ConvArgs a, int RW) {
   const int wm = wave / WGN, wn = wave % WGN;
   const int HWo = a.Ho * a.Wo;
   const int rws = __builtin_ctz(RW);                      // RW is a power of two, RW % WTM == 0
-  const int RH = BM >> rws, RWP = RW + 2, NPIX = RH * RWP;
+  const int RH = BM >> rws, RWP = UPC ? RW / 2 + 2 : RW + 2, NPIX = RH * RWP;
   const int NA = ((NPIX + QM) / (QM + 1) * (QM + 1) + RPI - 1) / RPI;
   const TileId tl = xcd_tile();
   const int tiles_w = a.Wo >> rws;
@@ -1079,12 +1087,17 @@ conv3i_kernel(ConvArgs a, int RW) {
     const int R = SA::logical(P);
     a_ls[j] = SA::slot(R, lane % SLOTS) * VE;
     const int oy = R / RWP, iw = ow0 + (R - oy * RWP) - 1;
+    const int sw = (ow0 >> 1) + (R - oy * RWP) - 1;             // UPC: source column
 #pragma unroll
     for (int kh = 0; kh < KHN; ++kh) {
       const int ih = UPH ? oh0 + 2 * oy + kh + ph - 1 : oh0 + oy + kh - 1;
       int pix = -1;
-      if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win)
+      if (UPC) {
+        if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)sw < (unsigned)a.Ws)
+          pix = pixb + (ih >> 1) * a.Ws + sw;
+      } else if (R < NPIX && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win) {
         pix = pixb + (a.up ? (ih >> 1) : ih) * a.Ws + (a.up ? (iw >> 1) : iw);
+      }
       if constexpr ((FL & 2048) != 0) pix = pix >= 0 ? (pix & 255) : pix;   // diagnostic: L2-resident A rows
       a_pix[j][kh] = BUF ? (pix >= 0 ? (pix * a.ld1 + a_ls[j]) * ES : (int)OOB) : pix;
     }
@@ -1112,7 +1125,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
     for (int j = 0; j < RGX; ++j) {
       const int lrow = (wave + j * NW) * RPI + lane / SLOTS;
-      const int row = 3 * BN + lrow;
+      const int row = NBR * BN + lrow;
       r_ls[j] = SB::slot(row, lane % SLOTS) * VE;
       const int part = lrow / BN;
       const int n = n0 + wperm64(lrow % BN);
@@ -1130,10 +1143,15 @@ conv3i_kernel(ConvArgs a, int RW) {
   const int w2_bytes = BUF && RES && a.w2 ? a.Cout * a.Cin * nparts * ES : 0;
   // Fragment offsets (stage-relative bytes).
   const int lr = lane & 15, lg = lane >> 4;
-  int aoff[NF][KSTEPS], boff[3][TN][KSTEPS];
+  int aoff[NF][KSTEPS], boff[NTAP][TN][KSTEPS];
+  // UPC: wave wm = (row y, column parity cb, 64-column part jo) of the tile; its fragment base
+  // is shifted by cb so that tap t2 of tile i reads F[i + t2].
+  const int upr = UPC ? (RW / 2) / 64 : 1;                  // waves per (row, parity)
+  const int cy = UPC ? wm / (2 * upr) : 0, cb = UPC ? (wm % (2 * upr)) / upr : 0;
+  const int cjo = UPC ? (wm % upr) * 64 : 0;
   {
     const int t0 = wm * WTM;
-    const int R0 = (t0 >> rws) * RWP + (t0 & (RW - 1)) + TM * lr;
+    const int R0 = UPC ? cy * RWP + cjo + cb + TM * lr : (t0 >> rws) * RWP + (t0 & (RW - 1)) + TM * lr;
 #pragma unroll
     for (int s = 0; s < NF; ++s)
 #pragma unroll
@@ -1141,12 +1159,12 @@ conv3i_kernel(ConvArgs a, int RW) {
         aoff[s][ks] = SA::phys(R0 + s) * CK + (SA::slot(R0 + s, ks * 4 + lg) << 4);
   }
 #pragma unroll
-  for (int kw = 0; kw < 3; ++kw)
+  for (int kw = 0; kw < NTAP; ++kw)
 #pragma unroll
     for (int jn = 0; jn < TN; ++jn)
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks) {
-        const int row = kw * BN + wn * WTN + jn * 16 + lr;
+        const int row = (UPC ? 2 * cb + kw : kw) * BN + wn * WTN + jn * 16 + lr;
         boff[kw][jn][ks] = AROWS * CK + row * CK + (SB::slot(row, ks * 4 + lg) << 4);
       }
 
@@ -1163,7 +1181,7 @@ conv3i_kernel(ConvArgs a, int RW) {
       for (int j = 0; j < AGX; ++j)
         if (wave + j * NW < NA)                                  // wave-uniform
           buf_lds16(from1 ? a.x1 : a.x2, x_bytes, st + (wave + j * NW) * RPI * CK, a_pix[j][kh], soa);
-      const int sob = ((UPH ? 2 * ph + kh : kh) * 3 * a.Cin + ci0) * ES;
+      const int sob = ((UPH ? 2 * ph + kh : kh) * NBR * a.Cin + ci0) * ES;
 #pragma unroll
       for (int j = 0; j < BGX; ++j)
         if (BGX == BGN || wave + j * NW < NB)                    // wave-uniform
@@ -1172,7 +1190,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
         for (int j = 0; j < RGX; ++j)
           if ((wave + j * NW) * RPI < RROWS)                       // wave-uniform
-            buf_lds16(a.w2, w2_bytes, st + (AROWS + 3 * BN) * CK + (wave + j * NW) * RPI * CK, r_ls[j], ci0 * ES);
+            buf_lds16(a.w2, w2_bytes, st + (AROWS + NBR * BN) * CK + (wave + j * NW) * RPI * CK, r_ls[j], ci0 * ES);
       }
       return;
     }
@@ -1191,7 +1209,7 @@ conv3i_kernel(ConvArgs a, int RW) {
 #pragma unroll
     for (int j = 0; j < BGX; ++j) {
       if (BGX == BGN || wave + j * NW < NB) {                   // wave-uniform
-        const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + (UPH ? 2 * ph + kh : kh) * 3 * a.Cin + ci0 + b_ls[j])
+        const char* src = b_ptr[j] ? reinterpret_cast<const char*>(b_ptr[j] + (UPH ? 2 * ph + kh : kh) * NBR * a.Cin + ci0 + b_ls[j])
                                    : zero;
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
                                          (lds_void_t*)(st + AROWS * CK + (wave + j * NW) * RPI * CK),
@@ -1204,7 +1222,7 @@ conv3i_kernel(ConvArgs a, int RW) {
         if ((wave + j * NW) * RPI < RROWS) {                        // wave-uniform
           const char* src = r_ptr[j] ? reinterpret_cast<const char*>(r_ptr[j] + ci0 + r_ls[j]) : zero;
           __builtin_amdgcn_global_load_lds(
-              (gbl_void_t*)src, (lds_void_t*)(st + (AROWS + 3 * BN) * CK + (wave + j * NW) * RPI * CK), 16, 0, 0);
+              (gbl_void_t*)src, (lds_void_t*)(st + (AROWS + NBR * BN) * CK + (wave + j * NW) * RPI * CK), 16, 0, 0);
         }
       }
     }
@@ -1239,7 +1257,7 @@ conv3i_kernel(ConvArgs a, int RW) {
           u32x4 fr[TN];
 #pragma unroll
           for (int jn = 0; jn < TN; ++jn) {
-            const int row = 3 * BN + pt * BN + wn * WTN + jn * 16 + lr;
+            const int row = NBR * BN + pt * BN + wn * WTN + jn * 16 + lr;
             fr[jn] = *reinterpret_cast<const u32x4*>(st + AROWS * CK + row * CK + (SB::slot(row, ks * 4 + lg) << 4));
           }
 #pragma unroll
@@ -1248,7 +1266,7 @@ conv3i_kernel(ConvArgs a, int RW) {
             for (int jn = 0; jn < TN; ++jn) Mma<T>::run(accR[i][jn], fr[jn], fa[i + 1]);
         }
       }
-      if constexpr (FL & 2) {
+      if constexpr ((FL & 2) && !UPC) {
         u32x4 fb[3][TN];
 #pragma unroll
         for (int kw = 0; kw < 3; ++kw)
@@ -1267,7 +1285,7 @@ conv3i_kernel(ConvArgs a, int RW) {
       }
       if constexpr (FL & 4) __builtin_amdgcn_s_setprio(1);   // MFMA phase ahead of the
 #pragma unroll                                                  // other block's DMA issue
-      for (int kw = 0; kw < 3; ++kw) {
+      for (int kw = 0; kw < NTAP; ++kw) {
         u32x4 fb[TN];
 #pragma unroll
         for (int jn = 0; jn < TN; ++jn) fb[jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
@@ -1309,8 +1327,11 @@ conv3i_kernel(ConvArgs a, int RW) {
   EpiPref<TM> pref;
   const int rm_base = b * HWo + oh0 * a.Wo + ow0;
   const int rstride = UPH ? 2 * a.Wo : a.Wo;              // output row stride of the tile
+  // UPC: the wave's pixel t is output column ow0 + 2 (cjo + t) + cb of row oh0 + 2 cy.
+  const int upc_base = b * HWo + (oh0 + 2 * cy) * a.Wo + ow0 + 2 * cjo + cb;
   auto pixf = [&](int i) {
     const int t = wm * WTM + TM * lr + i;
+    if constexpr (UPC) return (size_t)(upc_base + 2 * (TM * lr + i));
     return (size_t)(rm_base + (t >> rws) * rstride + (t & ((1 << rws) - 1)));
   };
   auto step = [&](int c, auto khc) {
@@ -1363,8 +1384,13 @@ conv3i_kernel(ConvArgs a, int RW) {
     // FL bit 12: fp8 output (ConvArgs::ys8, q8_store) — the fp8 handles' block1 with a fused
     // res_conv, whose y2 stays 16-bit.
     constexpr bool Q8 = (FL & 4096) != 0;
-    if (pre_ok) epi_regs16<T, TM, false, true, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
-    else epi_regs16<T, TM, false, false, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
+    if constexpr (UPC) {
+      if (pre_ok) epi_regs16<T, TM, false, true, Q8>(a, acc, bi, nb, b, pixf, &pref, el);
+      else epi_regs16<T, TM, false, false, Q8>(a, acc, bi, nb, b, pixf, nullptr, el);
+    } else {
+      if (pre_ok) epi_regs16<T, TM, false, true, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, &pref, el);
+      else epi_regs16<T, TM, false, false, Q8>(a, acc, bi, nb, b, [&](int i) { return (size_t)rm(wm * WTM + TM * lr + i); }, nullptr, el);
+    }
     if constexpr (RES) {
       // y2 = accR (+ bias2): lane holds channels nb .. nb+15 of pixel rows i (as epi_regs16).
       T* y2 = reinterpret_cast<T*>(a.y2);
@@ -1408,6 +1434,9 @@ bool conv3i_try(const ConvArgs& a, hipStream_t st) {
     if (!a.y2 || !a.w2) return false;
   if constexpr ((FL & 8192) != 0) {   // row-phase upsample tiles: one parity per tile
     if (!a.up || !a.uph || a.Ho % (2 * (BM / RW))) return false;
+    // column-phase too (FL bit 14): uph == 2, K = 16 Cin, rows of >= 128 output pixels
+    if (((FL & 16384) != 0) != (a.uph == 2)) return false;
+    if ((FL & 16384) && RW < 128) return false;
   } else if (a.uph) {
     return false;
   }
@@ -2078,9 +2107,11 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         if constexpr (sizeof(T) == 2) {
           // Buffer-resource DMA (FL bit 10) first; the flat-address form takes what it rejects.
           const int nb = g_conv3_buf ? 1024 : 0;
-          if (a.uph) {                                // row-phase upsample conv (conv_uph_ok)
-            if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 8192>(a, st)) return;
-            if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192>(a, st)) return;
+          if (a.uph) {                                // row- (and column-) phase upsample conv (conv_uph_ok)
+            if (a.uph == 2 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 8192 | 16384>(a, st)) return;
+            if (a.uph == 2 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192 | 16384>(a, st)) return;
+            if (a.uph == 1 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 8192>(a, st)) return;
+            if (a.uph == 1 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192>(a, st)) return;
             abort();
           }
           if (a.ys8) {                                // fp8 output (conv_q8out_ok): fused-res tiles only

@@ -75,6 +75,8 @@ struct ConvW {
   // 16-bit handles, 3x3 convs over a 2x nearest-upsampled input: row-phase weights
   // [cout][4][3][cin] = (W0, W1+W2 | W0+W1, W2) (ConvArgs::uph).
   const void* wph = nullptr;
+  // ... and the row- and column-phase weights [cout][4 row sets][4 column sets][cin] (uph = 2).
+  const void* wpc = nullptr;
 };
 
 // ----------------------------------------------------------------------------- run context

@@ -90,7 +90,9 @@ struct ConvArgs {
   // Upsample, module_util.py:100-103): output row 2i+a reads source rows (i-1, i, i) for a = 0
   // and (i, i, i+1) for a = 1, so its three kernel rows collapse to two with summed weights.
   // uph = 1: w is [Cout][4 rows][3][Cin] = (W0, W1+W2 | W0+W1, W2), K = 12 Cin, and the v4 tiles
-  // hold output rows of one parity (2 kernel-row stages per chunk instead of 3).
+  // hold output rows of one parity (2 kernel-row stages per chunk instead of 3). uph = 2: the
+  // columns fold the same way (each wave one column parity, 2 taps over source pixels):
+  // w is [Cout][4 row sets][4 (column parity, tap)][Cin], K = 16 Cin (rows >= 128 pixels).
   int uph;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).

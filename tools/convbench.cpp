@@ -705,7 +705,8 @@ static int uph_check(int iters) {
     const int Ho = 2 * sh.Hs, Wo = 2 * sh.Ws, M = sh.B * Ho * Wo, C = sh.cin, N = sh.cout;
     uint32_t hs = 4242 + C;
     auto rnd = [&]() { hs = hs * 1664525u + 1013904223u; return ((hs >> 8) & 0xffff) / 65535.f - 0.5f; };
-    std::vector<bf16> xb((size_t)sh.B * sh.Hs * sh.Ws * C), wb((size_t)N * 9 * C), pb((size_t)N * 12 * C);
+    std::vector<bf16> xb((size_t)sh.B * sh.Hs * sh.Ws * C), wb((size_t)N * 9 * C), pb((size_t)N * 12 * C),
+        qb((size_t)N * 16 * C);
     std::vector<float> wf((size_t)N * 9 * C), bias(N);
     for (auto& v : xb) v = (bf16)(2.f * rnd());
     for (auto& v : wf) v = 0.05f * rnd();
@@ -719,7 +720,21 @@ static int uph_check(int iters) {
         d[k] = (bf16)w[k]; d[R + k] = (bf16)(w[R + k] + w[2 * R + k]);
         d[2 * R + k] = (bf16)(w[k] + w[R + k]); d[3 * R + k] = (bf16)w[2 * R + k];
       }
-    void *dx, *dw, *dp, *dz, *dy0, *dy1; float* db;
+    {
+      static const int lo[4] = {0, 1, 0, 2}, hi[4] = {0, 2, 1, 2};
+      for (int o = 0; o < N; ++o)
+        for (int rs = 0; rs < 4; ++rs)
+          for (int cs = 0; cs < 4; ++cs)
+            for (int c = 0; c < C; ++c) {
+              float v = 0.f;
+              for (int kh = lo[rs]; kh <= hi[rs]; ++kh)
+                for (int kw = lo[cs]; kw <= hi[cs]; ++kw) v += wf[(((size_t)o * 3 + kh) * 3 + kw) * C + c];
+              qb[(((size_t)o * 4 + rs) * 4 + cs) * C + c] = (bf16)v;
+            }
+    }
+    void *dx, *dw, *dp, *dq, *dz, *dy0, *dy1, *dy2; float* db;
+    CK(hipMalloc(&dq, qb.size() * 2)); CK(hipMalloc(&dy2, (size_t)M * N * 2));
+    CK(hipMemcpy(dq, qb.data(), qb.size() * 2, hipMemcpyHostToDevice));
     CK(hipMalloc(&dx, xb.size() * 2)); CK(hipMalloc(&dw, wb.size() * 2)); CK(hipMalloc(&dp, pb.size() * 2));
     CK(hipMalloc(&dz, 256)); CK(hipMalloc(&dy0, (size_t)M * N * 2)); CK(hipMalloc(&dy1, (size_t)M * N * 2));
     CK(hipMalloc(&db, N * 4));
@@ -733,16 +748,22 @@ static int uph_check(int iters) {
     a.Wo = Wo; a.Cout = N; a.K = 9 * C; a.w = dw; a.bias = db; a.zero = dz; a.y = dy0; a.ldy = N;
     ConvArgs u = a;
     u.w = dp; u.K = 12 * C; u.uph = 1; u.y = dy1;
+    ConvArgs u2 = a;
+    u2.w = dq; u2.K = 16 * C; u2.uph = 2; u2.y = dy2;
+    const bool col = conv_uph_ok(u2);
     if (!conv_uph_ok(u)) { printf("%-28s not eligible\n", sh.name); ++fails; continue; }
     conv<bf16>(a, 3, 3, 1, 1, 0);
     conv<bf16>(u, 3, 3, 1, 1, 0);
+    if (col) conv<bf16>(u2, 3, 3, 1, 1, 0);
     CK(hipDeviceSynchronize());
-    std::vector<bf16> y0((size_t)M * N), y1((size_t)M * N);
+    std::vector<bf16> y0((size_t)M * N), y1((size_t)M * N), y2((size_t)M * N);
     CK(hipMemcpy(y0.data(), dy0, y0.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(y1.data(), dy1, y1.size() * 2, hipMemcpyDeviceToHost));
-    double md = 0, mx = 0;
+    if (col) CK(hipMemcpy(y2.data(), dy2, y2.size() * 2, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0, md2 = 0;
     for (size_t i = 0; i < y0.size(); ++i) {
       md = std::max(md, std::fabs((double)bf2f(y1[i]) - bf2f(y0[i])));
+      if (col) md2 = std::max(md2, std::fabs((double)bf2f(y2[i]) - bf2f(y0[i])));
       mx = std::max(mx, std::fabs((double)bf2f(y0[i])));
     }
     hipEvent_t e0, e1;
@@ -757,13 +778,15 @@ static int uph_check(int iters) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       return ms * 1e3 / iters;
     };
-    double t0 = tm(a), t1 = tm(u);
+    double t0 = tm(a), t1 = tm(u), t2 = col ? tm(u2) : 0.0;
     t0 = std::min(t0, tm(a));
     t1 = std::min(t1, tm(u));
-    const bool ok = md / mx < 1e-2;
-    printf("%-28s plain %6.1f us, row-phase %6.1f us  check rel %.2e %s\n", sh.name, t0, t1, md / mx, ok ? "OK" : "FAIL");
+    if (col) t2 = std::min(t2, tm(u2));
+    const bool ok = md / mx < 1e-2 && md2 / mx < 1e-2;
+    printf("%-28s plain %6.1f us, row-phase %6.1f us, row+column %6.1f us  check rel %.2e / %.2e %s\n", sh.name, t0,
+           t1, t2, md / mx, md2 / mx, ok ? "OK" : "FAIL");
     fails += !ok;
-    for (void* p : {dx, dw, dp, dz, dy0, dy1, (void*)db}) CK(hipFree(p));
+    for (void* p : {dx, dw, dp, dq, dz, dy0, dy1, dy2, (void*)db}) CK(hipFree(p));
     CK(hipEventDestroy(e0)); CK(hipEventDestroy(e1));
   }
   return fails;
