@@ -920,7 +920,29 @@ struct UNetNet {
     mid2 = load_rb(P, "mid_block2.", mid, mid);
     fin = load_rb(P, "final_res_block.", 2 * nf, nf, /*dual_res=*/split_edges);
     final_conv = P.conv_dual("final_conv.weight", cfg.out_nc, nf, 3, 3, "final_conv.bias");
+    // Every ResBlock's time MLP (SiLU, Linear(tdim, 2 dout)) reads the same embedding, so the
+    // per-call tables take them as ONE small_linear over the weights concatenated in ss_off
+    // order (each output is the same per-output dot product as a separate call's).
+    mw_all = mb_all = nullptr;
+    std::vector<const RB*> rbs;
+    for (auto& L : downs) { rbs.push_back(&L.b1); rbs.push_back(&L.b2); }
+    for (auto& L : ups) { rbs.push_back(&L.b1); rbs.push_back(&L.b2); }
+    rbs.push_back(&mid1); rbs.push_back(&mid2); rbs.push_back(&fin);
+    bool all = ss_total > 0;
+    for (const RB* rb : rbs) all = all && rb->mw && rb->mb;
+    if (all) {
+      float* W = (float*)P.pool.alloc((size_t)ss_total * tdim * 4);
+      float* bb = (float*)P.pool.alloc((size_t)ss_total * 4);
+      for (const RB* rb : rbs) {
+        HIP_OK(hipMemcpy(W + (size_t)rb->ss_off * tdim, rb->mw, (size_t)2 * rb->dout * tdim * 4, hipMemcpyDeviceToDevice));
+        HIP_OK(hipMemcpy(bb + rb->ss_off, rb->mb, (size_t)2 * rb->dout * 4, hipMemcpyDeviceToDevice));
+      }
+      mw_all = W;
+      mb_all = bb;
+    }
   }
+  const float* mw_all = nullptr;       // [ss_total][tdim]: all ResBlock time-MLP weights
+  const float* mb_all = nullptr;
 
   // ----------------------------------------------------------------- per-call tables
   // ss_all[(i*B + b)*ss_total + off ...]: ResBlock (scale, shift) for step i, image b, whose
@@ -955,9 +977,15 @@ struct UNetNet {
         small_linear(temb, tdim, rb.mw, rb.mb, ss_all + rb.ss_off, ss_total, R, tdim,
                      2 * rb.dout, ACT_SILU, ACT_NONE, nullptr, 0, 1, r.st);
     };
-    for (auto& L : downs) { rbt(L.b1); rbt(L.b2); }
-    for (auto& L : ups) { rbt(L.b1); rbt(L.b2); }
-    rbt(mid1); rbt(mid2); rbt(fin);
+    if (mw_all) {
+      if (!r.dry)
+        small_linear(temb, tdim, mw_all, mb_all, ss_all, ss_total, R, tdim, ss_total, ACT_SILU, ACT_NONE, nullptr, 0, 1,
+                     r.st);
+    } else {
+      for (auto& L : downs) { rbt(L.b1); rbt(L.b2); }
+      for (auto& L : ups) { rbt(L.b1); rbt(L.b2); }
+      rbt(mid1); rbt(mid2); rbt(fin);
+    }
     auto stc = [&](const Attn& a) {
       if (!a.st) return;
       const int C = a.s.pin.cout;
@@ -1286,7 +1314,9 @@ struct UNetNet {
 template <typename T>
 struct VitNet {
   struct Block { const float *l1w, *l1b, *l2w, *l2b; ConvW qkv, out, fc, proj; };
-  struct Tower { ConvW conv1; const float *cls, *pos, *prew, *preb, *postw, *postb, *projT;
+  // conv1g: the patch conv as a GEMM over im2col rows (K = 3 P P, stride == kernel), when K
+  // fits the GEMM tiles; conv1 the direct conv otherwise.
+  struct Tower { ConvW conv1, conv1g; const float *cls, *pos, *prew, *preb, *postw, *postb, *projT;
                  std::vector<Block> blocks; std::vector<ConvW> zero; };
   // CLIP text tower (model.py:203-211, 237-249): token / positional embeddings (fp32 tables),
   // causal ResidualAttentionBlocks, ln_final, text_projection (transposed, fp32).
@@ -1348,7 +1378,20 @@ struct VitNet {
   }
   Tower load_tower(Packer<T>& Pk, const std::string& p, bool control) {
     Tower t;
-    t.conv1 = Pk.conv(p + "conv1.weight", D, 3, P, P);
+    std::vector<float> pk;
+    t.conv1 = Pk.conv(p + "conv1.weight", D, 3, P, P, "", false, 0, &pk);
+    const int K = 3 * P * P, cp = t.conv1.cin;
+    if (K % 64 == 0 && !pk.empty() && !(getenv("DAC_VIT_GEMM") && atoi(getenv("DAC_VIT_GEMM")) == 0)) {
+      // [D][P][P][cin_pad] -> [D][P][P][3]: the same weights, the padding channels dropped.
+      std::vector<float> q((size_t)D * K);
+      for (size_t o = 0; o < (size_t)D; ++o)
+        for (int t2 = 0; t2 < P * P; ++t2)
+          for (int c = 0; c < 3; ++c) q[(o * P * P + t2) * 3 + c] = pk[(o * P * P + t2) * cp + c];
+      ConvW& g = t.conv1g;
+      g.cout = D; g.cin = g.cin_real = K; g.kh = g.kw = 1;
+      g.w = Pk.upload_T(q, p + "conv1.weight", P * P, 3);
+      Pk.make_fp8(g, q, D, K);
+    }
     t.cls = Pk.f32(p + "class_embedding", {D});
     t.pos = Pk.f32(p + "positional_embedding", {L, D});
     t.prew = Pk.f32(p + "ln_pre.weight", {D});
@@ -1408,11 +1451,17 @@ struct VitNet {
   }
   void tower(Run& r, const Tower& tw, const void* xin, int B, bool control,
              std::vector<const void*>* hid_out, const std::vector<const void*>* hid_in,
-             float* out) {
+             float* out, bool gemm) {
     constexpr int VE = sizeof(T) == 2 ? 8 : 4;
     const size_t Mt = (size_t)B * L;
     T* patch = r.alloc<T>((size_t)B * G * G * D);
-    conv_call<T>(r, tw.conv1, xin, VE, VE, nullptr, 0, B, S, S, 0, P, 0, patch, D, Epi());
+    if (gemm) {
+      // xin holds the im2col rows (encode): one GEMM over B * G^2 rows, K = 3 P P.
+      const int K = 3 * P * P;
+      conv_call<T>(r, tw.conv1g, xin, K, K, nullptr, 0, B, G * G, 1, 0, 1, 0, patch, D, Epi());
+    } else {
+      conv_call<T>(r, tw.conv1, xin, VE, VE, nullptr, 0, B, S, S, 0, P, 0, patch, D, Epi());
+    }
     T* tok = r.alloc<T>(Mt * D);
     if (!r.dry) vit_embed<T>(patch, tw.cls, tw.pos, tok, B, L, D, r.st);
     T* x = r.alloc<T>(Mt * D);
@@ -1441,11 +1490,15 @@ struct VitNet {
   // -> model.py:233-235), the clip tower alone.
   void encode(Run& r, const float* img, int B, float* ic, float* dc, bool control) {
     constexpr int VE = sizeof(T) == 2 ? 8 : 4;
-    T* xin = r.alloc<T>((size_t)B * S * S * VE);
-    if (!r.dry) vit_prep<T>(img, xin, B, S, r.st);
+    const bool gemm = main.conv1g.w && (!control || ctl.conv1g.w);
+    T* xin = r.alloc<T>(gemm ? (size_t)B * S * S * 3 : (size_t)B * S * S * VE);
+    if (!r.dry) {
+      if (gemm) vit_patches<T>(img, xin, B, S, P, r.st);
+      else vit_prep<T>(img, xin, B, S, r.st);
+    }
     std::vector<const void*> hid;
-    if (control) tower(r, ctl, xin, B, true, &hid, nullptr, dc);
-    tower(r, main, xin, B, false, nullptr, control ? &hid : nullptr, ic);
+    if (control) tower(r, ctl, xin, B, true, &hid, nullptr, dc, gemm);
+    tower(r, main, xin, B, false, nullptr, control ? &hid : nullptr, ic, gemm);
   }
 };
 

@@ -262,6 +262,9 @@ void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int 
 // ViT input: NCHW fp32 image -> NHWC T with channels padded to VE.
 template <typename T>
 void vit_prep(const float* img, void* x, int B, int S, hipStream_t st);
+// ViT stem input as GEMM rows: [B * (S/P)^2][3 P P] in (ky, kx, c) order (stride == kernel).
+template <typename T>
+void vit_patches(const float* img, void* x, int B, int S, int P, hipStream_t st);
 // tokens[b, 0] = cls + pos[0]; tokens[b, 1+p] = patch[b, p] + pos[1+p]
 template <typename T>
 void vit_embed(const void* patch, const float* cls, const float* pos, void* tok, int B, int L,

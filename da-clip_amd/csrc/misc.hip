@@ -292,6 +292,29 @@ void vit_prep(const float* img, void* x, int B, int S, hipStream_t st) {
   vit_prep_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(img, (T*)x, B, S);
 }
 
+// ViT stem as a GEMM: the patch conv has stride == kernel, so im2col is a pure gather.
+// x[(b * G*G + py * G + px) * K + (ky * P + kx) * 3 + c] = img[b][c][py P + ky][px P + kx],
+// K = 3 P P (the packed weight order [D][ky][kx][3]).
+template <typename T>
+__global__ void vit_patches_kernel(const float* img, T* x, int S, int P, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int K = 3 * P * P, G = S / P;
+  const int k = (int)(i % K);
+  const size_t row = i / K;
+  const int p = (int)(row % ((size_t)G * G));
+  const int b = (int)(row / ((size_t)G * G));
+  const int c = k % 3, kx = (k / 3) % P, ky = k / (3 * P);
+  const int py = p / G, px = p - py * G;
+  x[i] = from_f<T>(img[(((size_t)b * 3 + c) * S + py * P + ky) * S + px * P + kx]);
+}
+
+template <typename T>
+void vit_patches(const float* img, void* x, int B, int S, int P, hipStream_t st) {
+  const size_t n = (size_t)B * (S / P) * (S / P) * 3 * P * P;
+  vit_patches_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(img, (T*)x, S, P, n);
+}
+
 template <typename T>
 __global__ void vit_embed_kernel(const T* patch, const float* cls, const float* pos, T* tok,
                                  int L, int D, size_t n) {
@@ -333,6 +356,7 @@ void rows_to_f32(const void* x, int ld, float* y, int R, int D, hipStream_t st) 
                             const float*, const uint64_t*, uint32_t, StepCoef, int, int, int, \
                             hipStream_t);                                                     \
   template void vit_prep<T>(const float*, void*, int, int, hipStream_t);                      \
+  template void vit_patches<T>(const float*, void*, int, int, int, hipStream_t);               \
   template void vit_embed<T>(const void*, const float*, const float*, void*, int, int, int,   \
                              hipStream_t);                                                    \
   template void rows_to_f32<T>(const void*, int, float*, int, int, hipStream_t);
