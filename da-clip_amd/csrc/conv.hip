@@ -2,6 +2,7 @@
 // instantiated in conv_k3.hip / conv_k1.hip / conv_kx.hip.
 #include "common.h"
 #include "kernels.h"
+#include "conv_epi.h"
 
 namespace dac {
 
@@ -177,6 +178,59 @@ bool conv_uph_ok(const ConvArgs& a) {
   const int RW = conv3_rw_host(a, 256);
   return RW > 0 && RW % 64 == 0 && a.Ho % (2 * (256 / RW)) == 0 && (a.uph != 2 || RW >= 128);
 }
+
+// Split-K for 1x1 GEMMs whose 64x128 tile grid covers under half the CUs (the ViT and text
+// tower linears at M = B x L rows): enough K splits to fill the chip, each with >= 4 K tiles.
+// 0 = no split. Plain epilogues only (no row LayerNorm, folds, GEGLU or per-image weights).
+int conv_split_k(const ConvArgs& a, int elem_bytes) {
+  if (a.ln_g || a.lnf_cs || a.gna_stats || a.w_bstride || a.act == ACT_GEGLU || a.amode || a.cwrap || a.up ||
+      a.ys8 || a.xs8 || a.uph || !a.zero || a.Cin != a.K || a.Cout < 64)
+    return 0;
+  if (getenv("DAC_SPLITK") && atoi(getenv("DAC_SPLITK")) == 0) return 0;
+  const int BKE = 128 / elem_bytes;
+  if (a.K % BKE) return 0;
+  const long M = (long)a.B * a.Ho * a.Wo;
+  const long tiles = ((M + 63) / 64) * ((a.Cout + 127) / 128);
+  const int nk = a.K / BKE;
+  if (tiles >= 128 || nk < 8) return 0;
+  int s = (int)((256 + tiles - 1) / tiles);
+  s = s > nk / 4 ? nk / 4 : s;
+  s = s > 8 ? 8 : s;
+  return s >= 2 ? s : 0;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) conv_part_reduce_kernel(ConvArgs a, int M, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % a.Cout);
+  const int m = (int)(i / a.Cout);
+  float v = 0.f;
+  for (int z = 0; z < a.ksplit; ++z) v += a.part[((size_t)z * M + m) * a.Cout + c];
+  const int HWo = a.Ho * a.Wo, b = m / HWo;
+  // The register epilogues' fast path: bias folded into the shift, SiLU in the log2 domain.
+  float s = 1.f, h = 0.f;
+  if (a.ss) { s += a.ss[(size_t)b * a.ss_ld + c]; h = a.ss[(size_t)b * a.ss_ld + a.Cout + c]; }
+  const bool silu = a.act == ACT_SILU;
+  epi_fold(a.bias ? a.bias[c] : 0.f, s, h, silu);
+  v = fmaf(v, s, h);
+  if (silu) v = silu_log2(v);
+  else if (a.act == ACT_GELU) v = gelu_fast(v);
+  if (a.res1) v += to_f(reinterpret_cast<const T*>(a.res1)[(size_t)m * a.ldr1 + c]);
+  if (a.res2) v += to_f(reinterpret_cast<const T*>(a.res2)[(size_t)m * a.ldr2 + c]);
+  if (a.bbias) v += a.bbias[(size_t)b * a.bb_ld + c];
+  reinterpret_cast<T*>(a.y)[(size_t)m * a.ldy + c] = from_f<T>(v);
+}
+
+template <typename T>
+void conv_part_reduce(const ConvArgs& a, hipStream_t st) {
+  const int M = a.B * a.Ho * a.Wo;
+  const size_t n = (size_t)M * a.Cout;
+  conv_part_reduce_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(a, M, n);
+}
+template void conv_part_reduce<float>(const ConvArgs&, hipStream_t);
+template void conv_part_reduce<bf16>(const ConvArgs&, hipStream_t);
+template void conv_part_reduce<f16>(const ConvArgs&, hipStream_t);
 
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {

@@ -64,7 +64,8 @@ constexpr int epi_rows(int budget) {
 enum : int { EPI_GENERAL = 1, EPI_GEGLU = 2, EPI_GELU = 4, EPI_SCALAR = 8, EPI_MIN = 0, EPI_ALL = 15,
              EPI_LN = 16, EPI_SWAP = 32,   // EPI_SWAP: swapped operands + epi_regs16 (conv_impl.h)
              EPI_LNF = 64,                 // input LayerNorm folded into a 1x1 GEMM (ConvArgs::lnf_cs)
-             EPI_GNA = 128 };              // input GroupNorm applied in the A path (ConvArgs::gna_stats)
+             EPI_GNA = 128,                // input GroupNorm applied in the A path (ConvArgs::gna_stats)
+             EPI_PART = 256 };             // split-K partial sums to ConvArgs::part (no epilogue)
 
 // Per-channel epilogue terms of this lane's accumulator columns (bias, 1 + scale, shift) for a
 // tile inside image bimg; kernels that know bimg up front load them before the main loop.

@@ -395,7 +395,9 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   // EPI_GNA (1x1, swapped tiles): input GroupNorm applied to the A fragments from a per-channel
   // (scale, shift) table of this block's image, built in LDS behind the pipeline.
   constexpr bool GNA = (EPK & EPI_GNA) != 0;
-  constexpr int EPE = EPK & ~(EPI_LNF | EPI_GNA);
+  constexpr bool PART = (EPK & EPI_PART) != 0;
+  constexpr int EPE = EPK & ~(EPI_LNF | EPI_GNA | EPI_PART);
+  static_assert(!PART || (!LNF && !GNA && KH == 1 && KW == 1), "split-K: plain 1x1 GEMMs");
   static_assert(!LNF || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPK & EPI_SWAP)), "LN fold: 16-bit 1x1 swapped GEMMs");
   static_assert(!GNA || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPE & EPI_SWAP) && !LNF), "GN in A: 16-bit 1x1 swapped");
   constexpr bool SWAP = (EPE & EPI_SWAP) != 0;
@@ -451,7 +453,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     const int n = n0 + (SWAP ? (row & ~63) + wperm64(row & 63) : row);
     b_row[j] = n < a.Cout ? wgt + (size_t)n * a.K : nullptr;
   }
-  const int nk = (a.K + BKE - 1) / BKE;
+  // K tiles of this block: all, or split z's contiguous share (EPI_PART, grid z = ksplit).
+  const int nk_all = (a.K + BKE - 1) / BKE;
+  const int kt0 = PART ? (int)((long)tl.bz * nk_all / gridDim.z) : 0;
+  const int nk = PART ? (int)((long)(tl.bz + 1) * nk_all / gridDim.z) - kt0 : nk_all;
   // 1x1 with ConvArgs::dbuf: buffer-descriptor DMA. Per-lane byte offsets (pixel row x pitch +
   // slot; weight row x K + slot) computed once, the K advance in the scalar soffset, rows past
   // M / Cout (and K tiles past K) as out-of-range offsets that land zeros -- no 64-bit address
@@ -478,8 +483,8 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE;
-    const int k0 = kt * BKE;
-    const bool kv = k0 < a.K;
+    const int k0 = (kt0 + kt) * BKE;
+    const bool kv = kt < nk && k0 < a.K;
     if constexpr (KH == 7 && sizeof(T) == 2) {
       // Row-tap layout (kernel row padded to 8 taps, Cin = 8 = one 16-byte vector): K tile kt
       // is kernel row kh = kt, and logical slot s of a pixel row is tap kw = s (s = 7: zero).
@@ -712,6 +717,20 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e >> 2][e & 3] = rs[i] * fmaf(-mu[i], cs[e], acc[i][e >> 2][e & 3]);
     }
+  }
+  if constexpr (PART) {
+    // Raw partial sums: tile i row 4 lg + r is pixel m, column lr of tile j is channel n.
+    float* pz = a.part + (size_t)tl.bz * M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + 4 * lg + r, n = n0 + wn * WTN + j * 16 + lr;
+          if (m < M && n < a.Cout) pz[(size_t)m * a.Cout + n] = acc[i][j][r];
+        }
+    return;
   }
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
@@ -2272,6 +2291,14 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
           DAC_V2(64, 128, 2, 2, 2, 256)
         default: break;
       }
+    }
+    if constexpr (KH == 1) if (a.ksplit > 1 && a.part) {
+      // Split-K (conv_split_ok): 64x128 tiles, grid z = ksplit, then the reduce + epilogue pass.
+      if (a.ln_g || a.lnf_cs || a.gna_stats || batched || a.act == ACT_GEGLU) __builtin_trap();
+      dim3 g((Mg + 63) / 64, (a.Cout + 127) / 128, a.ksplit);
+      conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_PART><<<g, 256, 0, st>>>(a);
+      conv_part_reduce<T>(a, st);
+      return;
     }
     if constexpr (KH == 1) if (a.K <= BKE) {
       // One K tile (1x1 over 64 bf16 channels): no pipeline to fill, so a single small

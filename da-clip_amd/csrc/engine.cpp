@@ -596,6 +596,16 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
       fl += 2.0 * M * cw.cout * e.fuse1x1->cin_real;
     }
   }
+  // Split-K (the small-M 1x1 GEMMs: ViT / text tower linears): fp32 partials from the arena.
+  if (cw.kh == 1 && cw.kw == 1 && stride == 1 && pad == 0 && !use8 && !e.fuse1x1) {
+    ConvArgs q = a;
+    if (!r.zero) q.zero = &q;
+    const int ks = conv_split_k(q, (int)sizeof(T));
+    if (ks > 1) {
+      a.ksplit = ks;
+      a.part = r.alloc<float>((size_t)ks * (size_t)M * cw.cout);
+    }
+  }
   r.flops += fl;
   // Class 340: the fp8 ResBlock block2 (conv3q); an fp8-output block1 keeps its kernel's class.
   // Class 326: the row-phase upsample conv on v4 tiles (kept out of class 312's roofline).

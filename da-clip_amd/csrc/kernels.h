@@ -94,6 +94,12 @@ struct ConvArgs {
   // columns fold the same way (each wave one column parity, 2 taps over source pixels):
   // w is [Cout][4 row sets][4 (column parity, tap)][Cin], K = 16 Cin (rows >= 128 pixels).
   int uph;
+  // Split-K (1x1 GEMMs whose tile grid leaves the chip idle: the ViT / text linears, M = B x L):
+  // ksplit > 1 blocks along grid z each sum a contiguous range of K tiles into part
+  // [ksplit][M][Cout] (fp32, no epilogue); conv_part_reduce then sums them in fixed order and
+  // applies the epilogue (bias, activation, residuals) — set by the engine with the workspace.
+  int ksplit;
+  float* part;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
@@ -156,6 +162,11 @@ void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, c
 // (per output channel, tap and 32-channel half), on the block-scaled MFMA
 // v_mfma_scale_f32_16x16x128_f8f6f4; 16-bit output with the conv3w epilogue (bias, SiLU, res1).
 bool conv_q8out_ok(const ConvArgs& a);
+// Split-K (ConvArgs::ksplit / part): the 1x1 GEMM this engine call would split, and its second
+// pass (sum of the ksplit partials in order, then bias -> scale/shift -> activation -> residuals).
+int conv_split_k(const ConvArgs& a, int elem_bytes);
+template <typename T>
+void conv_part_reduce(const ConvArgs& a, hipStream_t st);
 // Row-phase upsample conv (ConvArgs::uph): the dispatcher has the kernel for this conv.
 bool conv_uph_ok(const ConvArgs& a);
 bool conv3q_ok(const ConvArgs& a);
