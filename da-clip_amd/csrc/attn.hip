@@ -238,11 +238,18 @@ template <int N> DEV void fkv_wait(int n) {
 //    subtraction; m is only moved when some score of the wave passes it by more than 2^FKV_TAU
 //    (p <= 2^8 fits T and the fp32 sums), the first chunk setting it. Exact: every p and every
 //    rescale uses the same m, and the final 1/sum cancels it.
+//  * JOINT (PRE, QG > 1): the wave's query groups walk a chunk together, in two 64-key halves,
+//    so each K / V fragment read from LDS serves every group (the 16-wave form otherwise
+//    re-reads them per group: half the LDS reads). m may move at either half (the first half of
+//    the first chunk sets it): the same exact-in-m formulation at a finer step.
+// The move test uses the lane's own max (any lane over TAU <=> some query's max over TAU); the
+// cross-lane reduction to each query's max runs only on the rare move path.
 constexpr float FKV_TAU = 8.f;
-template <typename T, int QG, int NW = FKV_NW, bool PRE = false>
+template <typename T, int QG, int NW = FKV_NW, bool PRE = false, bool JOINT = false>
 __global__ void __launch_bounds__(64 * NW) flash_kv_kernel(const T* __restrict__ qkv, T* o, int L,
                                                           int H, float scale) {
   static_assert(NW == 8 || NW == 16, "8 waves (two per SIMD) or 16 (four per SIMD)");
+  static_assert(!JOINT || PRE, "the joint group walk is built for the log2-domain form");
   constexpr int D = 32;
   extern __shared__ __attribute__((aligned(1024))) char fkv_smem[];
   char* sK = fkv_smem;
@@ -330,6 +337,72 @@ __global__ void __launch_bounds__(64 * NW) flash_kv_kernel(const T* __restrict__
     };
     // 8 waves: the chunk's K / V fragments are read once and serve all QG groups; 16 waves
     // (128 VGPRs) re-read them per group instead of holding 64 registers of them.
+    if constexpr (JOINT) {
+      // Two 64-key halves (32 S^T registers per group live at a time, not 64).
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool fst = first && h == 0;
+        f32x4 s[QG][4];
+        u32x4 pbu[QG][2];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const u32x4 kf = kload(4 * h + mi);
+#pragma unroll
+          for (int g = 0; g < QG; ++g) {
+            s[g][mi] = mneg[g];
+            Mma<T>::run(s[g][mi], kf, qf[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < QG; ++g) {
+          float lmax = s[g][0][0];
+#pragma unroll
+          for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lmax = fmaxf(lmax, s[g][mi][r]);
+          if (fst || __any(lmax > FKV_TAU)) {
+            const float tmax = red32_max(red16_max(lmax));
+            const float sh = fst ? tmax : fmaxf(tmax, 0.f);
+            if (!fst) {
+              const float corr = __builtin_amdgcn_exp2f(-sh);
+              lacc[g] *= corr;
+#pragma unroll
+              for (int dm = 0; dm < 2; ++dm) oacc[g][dm] *= corr;
+            }
+            mrun[g] += sh;
+            mneg[g] = f32x4{-mrun[g], -mrun[g], -mrun[g], -mrun[g]};
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+              s[g][mi] = mneg[g];
+              Mma<T>::run(s[g][mi], kload(4 * h + mi), qf[g]);
+            }
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            typename Vec8<T>::t pb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              pb[j] = (T)__builtin_amdgcn_exp2f(s[g][2 * s2][j]);
+              pb[4 + j] = (T)__builtin_amdgcn_exp2f(s[g][2 * s2 + 1][j]);
+            }
+            pbu[g][s2] = __builtin_bit_cast(u32x4, pb);
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+          for (int dm = 0; dm < 2; ++dm) {
+            const u32x4 vf = vload(2 * h + s2, dm);
+#pragma unroll
+            for (int g = 0; g < QG; ++g) Mma<T>::run(oacc[g][dm], vf, pbu[g][s2]);
+          }
+#pragma unroll
+          for (int g = 0; g < QG; ++g) Mma<T>::run(lacc[g], ones, pbu[g][s2]);
+        }
+      }
+      first = 0;
+      continue;
+    }
     constexpr bool HOIST = NW == 8;
     u32x4 kf[HOIST ? 8 : 1], vf[HOIST ? 4 : 1][2];
     if constexpr (HOIST) {
@@ -354,13 +427,12 @@ __global__ void __launch_bounds__(64 * NW) flash_kv_kernel(const T* __restrict__
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) tmax = fmaxf(tmax, s[mi][r]);
-      tmax = red16_max(tmax);
-      tmax = red32_max(tmax);
       if constexpr (PRE) {
         // s = score - m (log2 units). Rare case (the first chunk, or a score more than 2^TAU
         // above m): move m up to the chunk's max, rescale, and redo the S^T MFMAs from the new
         // -m, so both cases end in the same p = 2^s with no per-score subtraction.
         if (first || __any(tmax > FKV_TAU)) {
+          tmax = red32_max(red16_max(tmax));
           const float sh = first ? tmax : fmaxf(tmax, 0.f);
           if (!first) {
             const float corr = __builtin_amdgcn_exp2f(-sh);
@@ -382,6 +454,7 @@ __global__ void __launch_bounds__(64 * NW) flash_kv_kernel(const T* __restrict__
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[mi][r] = __builtin_amdgcn_exp2f(s[mi][r]);
       } else {
+        tmax = red32_max(red16_max(tmax));
         const float mnew = fmaxf(mrun[g], tmax * cs);
 #pragma unroll
         for (int mi = 0; mi < 8; ++mi)
@@ -589,7 +662,11 @@ int g_flash_kr = getenv("DAC_FLASH_KR") ? atoi(getenv("DAC_FLASH_KR")) : 0;
 // choice for the K/V-resident shapes (DAC_FKV16).
 int g_fkv16 = getenv("DAC_FKV16") ? atoi(getenv("DAC_FKV16")) : 0;
 
-template <typename T, int QG, int NW, bool PRE>
+// 1 (default): the 16-wave log2-domain kernel walks its two query groups jointly (DAC_FKV_JOINT;
+// 28.0 -> 26.6 us at C = 512, B = 8 standalone, tools/attn_bench.py).
+int g_fkv_joint = getenv("DAC_FKV_JOINT") ? atoi(getenv("DAC_FKV_JOINT")) : 1;
+
+template <typename T, int QG, int NW, bool PRE, bool JOINT = false>
 static void fkv_launch(const void* qkv, void* o, int B, int L, int H, float scale, hipStream_t st) {
   // > 64 KB of dynamic LDS must be opted into, once per (kernel, device).
   static std::atomic<uint64_t> done{0};
@@ -597,18 +674,19 @@ static void fkv_launch(const void* qkv, void* o, int B, int L, int H, float scal
   if (hipGetDevice(&dev) != hipSuccess || dev >= 64) dev = 63;
   const uint64_t bit = 1ull << dev;
   if (!(done.load(std::memory_order_acquire) & bit)) {
-    (void)hipFuncSetAttribute((const void*)flash_kv_kernel<T, QG, NW, PRE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)flash_kv_kernel<T, QG, NW, PRE, JOINT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               131072);
     done.fetch_or(bit, std::memory_order_acq_rel);
   }
   const dim3 g(L / (NW * 16 * QG), H, B);
-  flash_kv_kernel<T, QG, NW, PRE><<<g, 64 * NW, (size_t)L * 128, st>>>((const T*)qkv, (T*)o, L, H, scale);
+  flash_kv_kernel<T, QG, NW, PRE, JOINT><<<g, 64 * NW, (size_t)L * 128, st>>>((const T*)qkv, (T*)o, L, H, scale);
 }
 
 // variant: 0 = the dispatcher's choice (g_flash_old = DAC_FLASH_OLD selects the staged-tile
 // kernel process-wide, g_flash_kr = DAC_FLASH_KR the K/V-ring one), 1 = the staged-tile kernel,
 // 2 = the K/V-ring kernel (16-bit, L % 64 == 0), 3 = the 16-wave K/V-resident kernel (16-bit,
-// L % 256 == 0, L <= 1024). Passed explicitly by the op-level test hook, so no global state is
+// L % 256 == 0, L <= 1024), 4 = its two-group joint walk (16-bit, prescaled q, L % 512 == 0,
+// L <= 1024; else as 3). Passed explicitly by the op-level test hook, so no global state is
 // toggled per call. scale == 0: q was prescaled by 32^-0.5 * log2(e) (the engine's 16-bit
 // q|k|v weights), scores are already in log2 units.
 template <typename T>
@@ -616,7 +694,11 @@ void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale
   if constexpr (sizeof(T) == 2) {
     const bool pre = scale == 0.f;
     const bool kv = L % 128 == 0 && L <= 1024 && variant == 0 && !g_flash_old && !g_flash_kr;
-    if (L % 256 == 0 && L <= 1024 && (variant == 3 || (kv && (pre || g_fkv16)))) {
+    if (variant == 4 && pre && L % 512 == 0 && L <= 1024) {
+      fkv_launch<T, 2, 16, true, true>(qkv, o, B, L, H, scale, st);
+      return;
+    }
+    if (L % 256 == 0 && L <= 1024 && (variant == 3 || variant == 4 || (kv && (pre || g_fkv16)))) {
       // 16 waves x 2 query groups: the same 512 queries per block as the 8-wave QG = 4 kernel,
       // with four waves per SIMD to overlap one wave's S -> max -> exp -> PV chain; one query
       // group per wave (256 queries per block) when 512 would leave CUs idle. The log2-domain
@@ -624,7 +706,8 @@ void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale
       // 8-wave QG = 4 form spills with the extra -m operands).
       const bool two = L % 512 == 0 && (long)(L / 512) * H * B >= 256;
       if (pre) {
-        if (two) fkv_launch<T, 2, 16, true>(qkv, o, B, L, H, scale, st);
+        if (two && g_fkv_joint) fkv_launch<T, 2, 16, true, true>(qkv, o, B, L, H, scale, st);
+        else if (two) fkv_launch<T, 2, 16, true>(qkv, o, B, L, H, scale, st);
         else fkv_launch<T, 1, 16, true>(qkv, o, B, L, H, scale, st);
       } else {
         if (two) fkv_launch<T, 2, 16, false>(qkv, o, B, L, H, scale, st);

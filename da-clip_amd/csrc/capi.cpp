@@ -283,9 +283,9 @@ int dac_op_attention(const void* qkv, void* out, int B, int L, int H, int dtype,
   const bool pre = (variant & DAC_ATTN_Q_PRESCALED) != 0;
   variant &= ~DAC_ATTN_Q_PRESCALED;
   if (!qkv || !out || B <= 0 || L <= 0 || H <= 0 ||
-      (dtype != DAC_F32 && dtype != DAC_BF16 && dtype != DAC_F16) || variant < 0 || variant > 3 ||
+      (dtype != DAC_F32 && dtype != DAC_BF16 && dtype != DAC_F16) || variant < 0 || variant > 4 ||
       (variant == 2 && (dtype == DAC_F32 || L % 64)) ||
-      (variant == 3 && (dtype == DAC_F32 || L % 256 || L > 1024)))
+      (variant >= 3 && (dtype == DAC_F32 || L % 256 || L > 1024)))
     return DAC_E_ARG;
   const float scale = pre ? 0.f : 1.f / std::sqrt(32.f);
   const hipStream_t st = (hipStream_t)stream;

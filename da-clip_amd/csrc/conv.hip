@@ -181,16 +181,19 @@ bool conv_uph_ok(const ConvArgs& a) {
 
 // Split-K for 1x1 GEMMs whose 64x128 tile grid covers under half the CUs (the ViT and text
 // tower linears at M = B x L rows): enough K splits to fill the chip, each with >= 4 K tiles.
-// 0 = no split. Plain epilogues only (no row LayerNorm, folds, GEGLU or per-image weights).
-int conv_split_k(const ConvArgs& a, int elem_bytes) {
+// The split count is a function of `rows` = ONE image's rows (L), never of the batch: the
+// partial sums' order then does not depend on what else is in the batch, so an image's result
+// is bit-identical in any batch / shard. 0 = no split. Plain epilogues only (no row LayerNorm,
+// folds, GEGLU or per-image weights).
+int conv_split_k(const ConvArgs& a, int elem_bytes, long rows) {
   if (a.ln_g || a.lnf_cs || a.gna_stats || a.w_bstride || a.act == ACT_GEGLU || a.amode || a.cwrap || a.up ||
       a.ys8 || a.xs8 || a.uph || !a.zero || a.Cin != a.K || a.Cout < 64)
     return 0;
   if (getenv("DAC_SPLITK") && atoi(getenv("DAC_SPLITK")) == 0) return 0;
   const int BKE = 128 / elem_bytes;
   if (a.K % BKE) return 0;
-  const long M = (long)a.B * a.Ho * a.Wo;
-  const long tiles = ((M + 63) / 64) * ((a.Cout + 127) / 128);
+  if (rows <= 0) return 0;
+  const long tiles = ((rows + 63) / 64) * ((a.Cout + 127) / 128);
   const int nk = a.K / BKE;
   if (tiles >= 128 || nk < 8) return 0;
   int s = (int)((256 + tiles - 1) / tiles);

@@ -597,10 +597,10 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     }
   }
   // Split-K (the small-M 1x1 GEMMs: ViT / text tower linears): fp32 partials from the arena.
-  if (cw.kh == 1 && cw.kw == 1 && stride == 1 && pad == 0 && !use8 && !e.fuse1x1) {
+  if (e.split_rows > 0 && cw.kh == 1 && cw.kw == 1 && stride == 1 && pad == 0 && !use8 && !e.fuse1x1) {
     ConvArgs q = a;
     if (!r.zero) q.zero = &q;
-    const int ks = conv_split_k(q, (int)sizeof(T));
+    const int ks = conv_split_k(q, (int)sizeof(T), e.split_rows);
     if (ks > 1) {
       a.ksplit = ks;
       a.part = r.alloc<float>((size_t)ks * (size_t)M * cw.cout);
@@ -1365,24 +1365,29 @@ struct VitNet {
     T* a = r.alloc<T>(Mt * Dm);
     ln<T>(r, x, Dm, a, Dm, nullptr, 0, b.l1w, b.l1b, (int)Mt, Dm, 1e-5f);
     T* qkv = r.alloc<T>(Mt * 3 * Dm);
-    conv_call<T>(r, b.qkv, a, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, qkv, 3 * Dm, Epi());
+    Epi eq;
+    eq.split_rows = Ls;
+    conv_call<T>(r, b.qkv, a, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, qkv, 3 * Dm, eq);
     T* o = r.alloc<T>(Mt * Dm);
     r.flops += 4.0 * Bs * (double)Ls * Ls * Dm;
     if (!r.dry) small_mha<T>(qkv, o, Bs, Ls, Hm, Dm / Hm, causal, r.st);
     T* x2 = r.alloc<T>(Mt * Dm);
     Epi e1;
     e1.res1 = x; e1.ldr1 = Dm;
+    e1.split_rows = Ls;
     conv_call<T>(r, b.out, o, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x2, Dm, e1);
     T* a2 = r.alloc<T>(Mt * Dm);
     ln<T>(r, x2, Dm, a2, Dm, nullptr, 0, b.l2w, b.l2b, (int)Mt, Dm, 1e-5f);
     T* f = r.alloc<T>(Mt * mlpw);
     Epi eg;
     eg.act = ACT_GELU;
+    eg.split_rows = Ls;
     conv_call<T>(r, b.fc, a2, Dm, Dm, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, f, mlpw, eg);
     T* x3 = r.alloc<T>(Mt * Dm);
     Epi e3;
     e3.res1 = x2; e3.ldr1 = Dm;
     if (res2) { e3.res2 = res2; e3.ldr2 = Dm; }
+    e3.split_rows = Ls;
     conv_call<T>(r, b.proj, f, mlpw, mlpw, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, x3, Dm, e3);
     return x3;
   }
@@ -1468,7 +1473,9 @@ struct VitNet {
     if (gemm) {
       // xin holds the im2col rows (encode): one GEMM over B * G^2 rows, K = 3 P P.
       const int K = 3 * P * P;
-      conv_call<T>(r, tw.conv1g, xin, K, K, nullptr, 0, B, G * G, 1, 0, 1, 0, patch, D, Epi());
+      Epi es;
+      es.split_rows = G * G;
+      conv_call<T>(r, tw.conv1g, xin, K, K, nullptr, 0, B, G * G, 1, 0, 1, 0, patch, D, es);
     } else {
       conv_call<T>(r, tw.conv1, xin, VE, VE, nullptr, 0, B, S, S, 0, P, 0, patch, D, Epi());
     }
@@ -1481,7 +1488,9 @@ struct VitNet {
                     hid_in ? (*hid_in)[layers - 1 - l] : nullptr);        // control.pop()
       if (control) {
         T* hz = r.alloc<T>(Mt * D);
-        conv_call<T>(r, tw.zero[l], x3, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, hz, D, Epi());
+        Epi ez;
+        ez.split_rows = L;
+        conv_call<T>(r, tw.zero[l], x3, D, D, nullptr, 0, 1, 1, (int)Mt, 0, 1, 0, hz, D, ez);
         hid_out->push_back(hz);
       }
       x = x3;

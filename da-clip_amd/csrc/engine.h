@@ -150,6 +150,9 @@ struct Epi {
   // these exponents; xs8 = the input x1 is e4m3 with these exponents (conv3q, weights cw.q8w).
   uint8_t* ys8 = nullptr;
   const uint8_t* xs8 = nullptr;
+  // 1x1 GEMMs that may split K (conv_split_k): the rows of ONE image (tower token count); the
+  // split is chosen from it, never from the batch, so results stay batch-invariant. 0 = no split.
+  int split_rows = 0;
 };
 
 template <typename T>

@@ -164,7 +164,7 @@ void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, c
 bool conv_q8out_ok(const ConvArgs& a);
 // Split-K (ConvArgs::ksplit / part): the 1x1 GEMM this engine call would split, and its second
 // pass (sum of the ksplit partials in order, then bias -> scale/shift -> activation -> residuals).
-int conv_split_k(const ConvArgs& a, int elem_bytes);
+int conv_split_k(const ConvArgs& a, int elem_bytes, long rows);
 template <typename T>
 void conv_part_reduce(const ConvArgs& a, hipStream_t st);
 // Row-phase upsample conv (ConvArgs::uph): the dispatcher has the kernel for this conv.

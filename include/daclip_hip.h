@@ -177,7 +177,9 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
  * of 32), out [B*L, H*32], both in `dtype` (DAC_F32 / DAC_BF16) on the current device;
  * scale = 32^-0.5. variant: 0 = the dispatcher's choice, 1 = the staged-tile kernel,
  * 2 = the K/V-ring kernel (16-bit dtypes, L % 64 == 0; DAC_E_ARG otherwise), 3 = the 16-wave
- * K/V-resident kernel (16-bit dtypes, L % 256 == 0, L <= 1024; DAC_E_ARG otherwise).
+ * K/V-resident kernel (16-bit dtypes, L % 256 == 0, L <= 1024; DAC_E_ARG otherwise), 4 = the
+ * same with its two query groups per wave walked jointly (prescaled q and L % 512 == 0; other
+ * shapes run as 3; same constraints as 3).
  * variant | DAC_ATTN_Q_PRESCALED: q was multiplied by 32^-0.5 * log2(e) before rounding (as the
  * 16-bit handles' q|k|v weights are), so scores come out in log2 units.
  * dtype: DAC_F32, DAC_BF16 or DAC_F16. */

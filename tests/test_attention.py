@@ -47,7 +47,7 @@ def test_attention_16bit_matches_fp32_reference(B, L, H, dt):
     ref = _ref(qkv, B, L, H)
     variants = (0, 1, 2) if L % 64 == 0 else (0, 1)
     if L % 256 == 0 and L <= 1024:
-        variants += (3,)
+        variants += (3, 4)
     # The engine's 16-bit q|k|v weights emit q already times 32^-0.5 log2(e) (one rounding):
     # the kernels then take scores in log2 units (DAC_ATTN_Q_PRESCALED).
     pre = qkv.float()
@@ -92,7 +92,7 @@ def test_attention_kernels_agree_and_handle_peaky_scores():
     back = pre.float()
     back.view(B, L, 3, H, 32)[:, :, 0] /= f
     ref_pre = _ref(back, B, L, H)
-    for variant in (0, 3):
+    for variant in (0, 3, 4):                   # 4: the two-group joint walk (half-chunk moves)
         e = _run(pre, B, L, H, _lib.DAC_BF16, variant | _lib.DAC_ATTN_Q_PRESCALED).float()
         assert torch.isfinite(e).all()
         assert (e - ref_pre).abs().max().item() / ref_pre.abs().max().item() < 1e-2, variant

@@ -230,6 +230,22 @@ def test_daclip_encode_matches_reference(golden, name, dt):
     assert rel(dc.cpu().numpy(), g["degra_context"]) < tol
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_daclip_encode_batch_invariant(dt):
+    """Each image's contexts are bit-identical whether it is encoded alone or in a batch (the
+    sharded bench encodes per shard): the tower GEMMs' split-K depth is chosen per image's token
+    count, never from the batch (conv.hip conv_split_k)."""
+    from daclip_amd import arch, synth
+    from daclip_amd.open_clip import DaCLIP
+    m = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=dt)
+    m.load_synthetic(seed=0)
+    img = T(synth.synth_noise((6, 3, 224, 224), seed=5, tag="encb"))
+    ic, dc = m.encode_image(img, control=True)
+    for i in (0, 3, 5):
+        ic1, dc1 = m.encode_image(img[i:i + 1], control=True)
+        assert torch.equal(ic[i:i + 1], ic1) and torch.equal(dc[i:i + 1], dc1), i
+
+
 def test_strict_loading_errors(unet_sd):
     from daclip_amd.unet import ConditionalUNet
     m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True)

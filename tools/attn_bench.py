@@ -19,7 +19,7 @@ for (B, L, H), (tdt, code) in [(s, d) for s in [(8, 1024, 16), (8, 1024, 8)]
     pre = qkv.float()
     pre.view(B * L, 3, H * 32)[:, 0] *= 32 ** -0.5 * 1.4426950408889634
     pre = pre.to(tdt)
-    for variant in (0, 1, 2, 3, 8, 11):          # 8 | v: q prescaled (the engine's form)
+    for variant in (0, 1, 2, 3, 8, 11, 12):          # 8 | v: q prescaled (the engine's form)
         q = pre if variant & 8 else qkv
         args = (ctypes.c_void_p(q.data_ptr()), ctypes.c_void_p(out.data_ptr()), B, L, H, code, variant, st)
         for _ in range(3):
