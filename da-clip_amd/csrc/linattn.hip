@@ -247,6 +247,12 @@ template void linear_attention_weff<f16>(const void*, const float*, void*, int, 
 // instead of x -> xn -> qkv (384 ch) -> k, v and a q round trip. The chunking depends only
 // on HW (la_chunks), so results stay batch- and shard-invariant.
 constexpr int LA_FPART = 4096 + 256;   // ctx | sum | max
+// la_proj_ctx's reference-max slack (natural-log units); DAC_LA_STALE=0: -inf, the max moves on
+// every tile (the exact running max of round 3).
+static float la_tau() {
+  static const float t = (getenv("DAC_LA_STALE") && atoi(getenv("DAC_LA_STALE")) == 0) ? -INFINITY : 5.5f;
+  return t;
+}
 
 // Reductions over the 16 lanes of a DPP row (the lanes holding one MFMA C-tile row): quad
 // xor 1, quad xor 2, half-row mirror, row mirror -- VALU only, no LDS round trip.
@@ -320,7 +326,7 @@ template <typename T, int C>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 64 ? 2 : 1, 2))) la_proj_ctx(const T* __restrict__ x, const float* __restrict__ g,
                                                    const T* __restrict__ w,
                                                    float* __restrict__ part, int HW, int nc, int CH,
-                                                   float eps) {
+                                                   float eps, float tau) {
   using K = LaCfg<T, C>;
   constexpr int VE = K::VE, TP = K::TP, PT = K::PT, KS = K::KS, KSTEP = K::KSTEP;
   __shared__ __attribute__((aligned(16))) char smem[K::SMEM];
@@ -439,7 +445,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
     // pt*16 + lg*4 + r, which is itself a valid MFMA operand layout (row = channel, k = those
     // pixels, the same pixel -> k map for P and V), so the context MFMA needs no LDS transpose.
     // Padding pixels are 0. Whole tiles (all but an image's last) skip the validity tests.
-    float sc[2];
+    // Stale reference max (16-bit types): m moves only when some k of the tile passes it by more
+    // than tau (la_tau(): p = exp(k - m) <= e^5.5 fits T and the fp32 sums); the partial's max is
+    // that reference, which la_combine_weff rescales like any other. Exact in m: every p and
+    // every rescale of a chunk use the same m. Skips the cross-lane max, the rescale factors'
+    // LDS broadcast and the context rescale on all tiles but the first (and rare movers).
+    float sc[2] = {1.f, 1.f};
+    bool resc = false;
     constexpr int PPK = KSTEP / 16;                       // pixel tiles per k-step: 2 bf16, 1 f32
     static_assert(PT % PPK == 0, "pixel tiles per k-step");
     u32x4 fp[2][PT / PPK], fv[2][PT / PPK];
@@ -453,12 +465,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (FULL || t0 + pt * 16 + lg * 4 + r < p1) m = fmaxf(m, acc[pt][jt][r]);
-        m = red16_max(m);
-        m = red32_max(m);
-        const float mn = fmaxf(mrun[jt], m);
-        sc[jt] = exp_t<T>(mrun[jt] - mn);                 // 0 on the first tile
-        mrun[jt] = mn;
-        srun[jt] *= sc[jt];
+        if (sizeof(T) == 4 || __any(m > mrun[jt] + tau)) {
+          m = red16_max(m);
+          m = red32_max(m);
+          const float mn = fmaxf(mrun[jt], m);
+          sc[jt] = exp_t<T>(mrun[jt] - mn);               // 0 on the first tile
+          mrun[jt] = mn;
+          srun[jt] *= sc[jt];
+          resc = true;
+        }
       }
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
@@ -489,16 +504,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
     if (t0 + TP <= p1) kpv(std::true_type{});
     else kpv(std::false_type{});
     // Broadcast the per-channel rescale factors to the ctx accumulator layout (row d).
-    if (lg == 0) { sm[lr] = sc[0]; sm[16 + lr] = sc[1]; }
-    wave_sync_lds();
+    if (resc) {                                           // wave-uniform
+      if (lg == 0) { sm[lr] = sc[0]; sm[16 + lr] = sc[1]; }
+      wave_sync_lds();
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float f = sm[i * 16 + lg * 4 + r];
+        for (int r = 0; r < 4; ++r) {
+          const float f = sm[i * 16 + lg * 4 + r];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) cacc[i][j][r] *= f;
-      }
+          for (int j = 0; j < 2; ++j) cacc[i][j][r] *= f;
+        }
+      wave_sync_lds();                                    // sm reads done before the next tile
+    }
     // ---- ctx[d][e] += sum_px P[d][px] V[e][px]
 #pragma unroll
     for (int kk = 0; kk < PT / PPK; ++kk)
@@ -506,7 +524,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) Mma<T>::run(cacc[i][j], fp[i][kk], fv[j][kk]);
-    wave_sync_lds();                                      // sm reads done before the next tile
     // ---- next tile: normalise the prefetched pixels into the other buffer.
     if (more) xstore(buf ^ 1);
     __syncthreads();
@@ -905,11 +922,11 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
   const int nc = la_chunks(B, HW), CH = la_chunk_px(HW, nc);
   float* part = ws;
   if (C == 64)
-    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
+    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else if (C == 128)
-    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
+    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else if constexpr (sizeof(T) == 2)
-    la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f);
+    la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else
     __builtin_trap();
   // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
