@@ -30,6 +30,20 @@ static int la_chunks(int /*B*/, int HW) {
   const int maxc = (HW + LA_TILE - 1) / LA_TILE;
   return nc < maxc ? nc : maxc;
 }
+// The fused pair (la_proj_ctx + la_combine_weff): fewer, longer chunks where the context pass
+// is per-block-overhead bound (rocprof sweep, fp16 bench, proj + combine per launch: C = 64 at
+// 256^2 41.2 -> 37.7 us with 64 chunks, C = 128 at 128^2 28.0 -> 25.0, C = 256 at 64^2 31.9 ->
+// 27.3 with 32); the 512^2 levels (Wild-IR, 2 images per GPU) keep 128 to fill the chip. A
+// function of (HW, C) only -- never of the batch -- and <= la_chunks() (the workspace bound).
+// DAC_LA_NC overrides it (8..128, tuning).
+static int la_fused_chunks(int HW, int C) {
+  static const int force = getenv("DAC_LA_NC") ? atoi(getenv("DAC_LA_NC")) : 0;
+  int nc = force > 0 ? (force < 8 ? 8 : force > 128 ? 128 : force) : C >= 256 ? 32 : HW >= 131072 ? 128 : 64;
+  const int maxc = (HW + LA_TILE - 1) / LA_TILE;
+  nc = nc < maxc ? nc : maxc;
+  const int lim = la_chunks(1, HW);
+  return nc < lim ? nc : lim;
+}
 static int la_chunk_px(int HW, int nc) {
   int ch = (HW + nc - 1) / nc;
   return (ch + LA_TILE - 1) / LA_TILE * LA_TILE;
@@ -245,7 +259,7 @@ template void linear_attention_weff<f16>(const void*, const float*, void*, int, 
 //                 LayerNorm over C (to_out.1) -> + x (Residual) -> y.
 // HBM traffic per image: x read twice, y written once (2 * HW * C elements in, HW * C out),
 // instead of x -> xn -> qkv (384 ch) -> k, v and a q round trip. The chunking depends only
-// on HW (la_chunks), so results stay batch- and shard-invariant.
+// on HW and C (la_fused_chunks), so results stay batch- and shard-invariant.
 constexpr int LA_FPART = 4096 + 256;   // ctx | sum | max
 // la_proj_ctx's reference-max slack (natural-log units); DAC_LA_STALE=0: -inf, the max moves on
 // every tile (the exact running max of round 3).
@@ -919,7 +933,7 @@ template <typename T>
 void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, const float* wout,
                             const float* bout, const float* gout, void* weff, void* y, int B, int HW,
                             int C, float* ws, hipStream_t st) {
-  const int nc = la_chunks(B, HW), CH = la_chunk_px(HW, nc);
+  const int nc = la_fused_chunks(HW, C), CH = la_chunk_px(HW, nc);
   float* part = ws;
   if (C == 64)
     la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
