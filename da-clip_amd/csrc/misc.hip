@@ -263,10 +263,54 @@ __global__ void sde_step_kernel(int mode, float* x, const float* mu, const T* ep
   x[i] = out;
 }
 
+// The loop form (eps = the final conv's NHWC output, ld channels a pixel): one thread per pixel
+// and all three channels, so eps is read as one contiguous run per pixel instead of three
+// scattered 2-byte reads from three planes' threads. Same per-element arithmetic, noise key and
+// output as sde_step_kernel (bit-identical).
+template <typename T>
+__global__ void sde_step_px_kernel(int mode, float* x, const float* mu, const T* eps, int ld, int Hp,
+                                   int Wp, const float* z, const uint64_t* seedp, uint32_t tag,
+                                   StepCoef c, int H, int W, size_t npx) {
+  const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= npx) return;
+  const int w = (int)(p % W);
+  const int h = (int)((p / W) % H);
+  const int b = (int)(p / ((size_t)W * H));
+  const T* ep = eps + (((size_t)b * Hp + h) * Wp + w) * ld;
+  float e3[3];
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) e3[ch] = to_f(ep[ch]);
+  const size_t plane = (size_t)H * W;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const size_t i = ((size_t)b * 3 + ch) * plane + (size_t)h * W + w;
+    const float e = e3[ch];
+    const float xv = x[i], m = mu[i];
+    const float zv = z ? z[i] : philox_normal(seedp[0], tag, i + seedp[1]);
+    float out;
+    if (mode == 0) {
+      const float x0 = ((xv - m) - c.sbar * e) * c.ea + m;                  // sde_utils.py:245-247
+      const float mean = c.t1 * (xv - m) + c.t2 * (x0 - m) + m;             // :205-213
+      out = mean + c.std * zv;                                              // :227-231
+    } else {
+      const float score = -e / c.sbar;                                      // :186-187
+      const float drift = (c.theta * (m - xv) - c.sigma2 * score) * c.dt;   // :177-178
+      out = xv - drift - c.sigma_sqrt_dt * zv;                              // :44-45, 183-184
+    }
+    x[i] = out;
+  }
+}
+
 template <typename T>
 void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
               const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
               int W, hipStream_t st) {
+  if (ld >= 3 && !(getenv("DAC_SDE_PX") && atoi(getenv("DAC_SDE_PX")) == 0)) {
+    const size_t npx = (size_t)B * H * W;
+    sde_step_px_kernel<T><<<(unsigned)((npx + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld, Hp, Wp,
+                                                                         z, seedp, tag, c, H, W, npx);
+    return;
+  }
   const size_t n = (size_t)B * 3 * H * W;
   sde_step_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld,
                                                                   Hp, Wp, z, seedp, tag, c, H, W, n);

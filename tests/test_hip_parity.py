@@ -93,6 +93,34 @@ def test_unet_batch_invariance_and_determinism_256(unets):
         assert torch.equal(one, both[i:i + 1])
 
 
+@pytest.mark.parametrize("mode", ["posterior", "sde"])
+def test_loop_sde_step_pixel_kernel_bit_identical(unet_sd, monkeypatch, mode):
+    """The loop's SDE update runs one thread per pixel (misc.hip sde_step_px_kernel); it must
+    give exactly the planar kernel's result (DAC_SDE_PX=0), device noise included."""
+    from daclip_amd import synth
+    from daclip_amd.sde import IRSDE
+    from daclip_amd.unet import ConditionalUNet
+    lq = T(synth.synth_images(2, 64, 64, seed=81))
+    tc = T(synth.synth_noise((2, 512), seed=82, tag="tc"))
+    ic = T(synth.synth_noise((2, 512), seed=83, tag="ic"))
+
+    def run():
+        m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype="fp16")
+        m.load_state_dict(unet_sd)
+        s = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+        s.set_model(m)
+        s.set_mu(lq)
+        if mode == "posterior":
+            return s.reverse_posterior(lq, T=3, text_context=tc, image_context=ic)
+        return s.reverse_sde(lq, T=3, text_context=tc, image_context=ic)
+    monkeypatch.setenv("DAC_SDE_PX", "0")
+    planar = run()
+    monkeypatch.delenv("DAC_SDE_PX")
+    px = run()
+    assert torch.isfinite(px).all()
+    assert torch.equal(px, planar)
+
+
 def test_unet_forward_256_fp32_vs_oracle(unets, unet_sd):
     from daclip_amd import synth
     from oracle import unet as OU
