@@ -238,7 +238,7 @@ template <int N> DEV void fkv_wait(int n) {
 //    subtraction; m is only moved when some score of the wave passes it by more than 2^FKV_TAU
 //    (p <= 2^8 fits T and the fp32 sums), the first chunk setting it. Exact: every p and every
 //    rescale uses the same m, and the final 1/sum cancels it.
-//  * JOINT (PRE, QG > 1): the wave's query groups walk a chunk together, in two 64-key halves,
+//  * JOINT (PRE): the wave's query groups walk a chunk together, in two 64-key halves,
 //    so each K / V fragment read from LDS serves every group (the 16-wave form otherwise
 //    re-reads them per group: half the LDS reads). m may move at either half (the first half of
 //    the first chunk sets it): the same exact-in-m formulation at a finer step.
@@ -706,8 +706,12 @@ void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale
       // 8-wave QG = 4 form spills with the extra -m operands).
       const bool two = L % 512 == 0 && (long)(L / 512) * H * B >= 256;
       if (pre) {
+        // One query group per wave takes the same walk (64-key halves) as the joint two-group
+        // kernel: the per-group arithmetic -- and so every output -- is then the same whichever
+        // of the two the batch size selects (batch- and shard-invariance).
         if (two && g_fkv_joint) fkv_launch<T, 2, 16, true, true>(qkv, o, B, L, H, scale, st);
         else if (two) fkv_launch<T, 2, 16, true>(qkv, o, B, L, H, scale, st);
+        else if (g_fkv_joint) fkv_launch<T, 1, 16, true, true>(qkv, o, B, L, H, scale, st);
         else fkv_launch<T, 1, 16, true>(qkv, o, B, L, H, scale, st);
       } else {
         if (two) fkv_launch<T, 2, 16, false>(qkv, o, B, L, H, scale, st);
@@ -718,7 +722,8 @@ void flash_attn_d32_v(const void* qkv, void* o, int B, int L, int H, float scale
     if (kv) {
       // K/V-resident kernel: 4 query groups per wave (512 queries per block) when that still
       // fills the chip, else 2 (or 1).
-      if (pre) fkv_launch<T, 1, FKV_NW, true>(qkv, o, B, L, H, scale, st);
+      if (pre && g_fkv_joint) fkv_launch<T, 1, FKV_NW, true, true>(qkv, o, B, L, H, scale, st);
+      else if (pre) fkv_launch<T, 1, FKV_NW, true>(qkv, o, B, L, H, scale, st);
       else if (L % 512 == 0 && (long)(L / 512) * H * B >= 256) fkv_launch<T, 4, FKV_NW, false>(qkv, o, B, L, H, scale, st);
       else if (L % 256 == 0) fkv_launch<T, 2, FKV_NW, false>(qkv, o, B, L, H, scale, st);
       else fkv_launch<T, 1, FKV_NW, false>(qkv, o, B, L, H, scale, st);

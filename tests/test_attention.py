@@ -98,6 +98,25 @@ def test_attention_kernels_agree_and_handle_peaky_scores():
         assert (e - ref_pre).abs().max().item() / ref_pre.abs().max().item() < 1e-2, variant
 
 
+def test_attention_one_and_two_group_kernels_bit_identical():
+    """The log2-domain K/V-resident kernels with one and with two query groups per wave (the
+    dispatcher picks by B * H, so by the batch) walk each 16-query group identically: outputs
+    are bit-identical, also when the reference max moves (peaky scores)."""
+    from daclip_amd import _lib
+    B, L, H = 2, 1024, 4
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for scale_k in (1.0, 6.0):
+        qkv = torch.randn(B * L, 3 * H * 32, device="cuda", generator=g)
+        qkv.view(B, L, 3, H, 32)[:, :, 1] *= scale_k * torch.linspace(0.2, 2.0, L, device="cuda").view(1, L, 1, 1)
+        qkv.view(B * L, 3, H * 32)[:, 0] *= 32 ** -0.5 * 1.4426950408889634
+        for tdt, code in ((torch.float16, _lib.DAC_F16), (torch.bfloat16, _lib.DAC_BF16)):
+            q = qkv.to(tdt)
+            one = _run(q, B, L, H, code, 3 | _lib.DAC_ATTN_Q_PRESCALED)     # B * H small: one group
+            two = _run(q, B, L, H, code, 4 | _lib.DAC_ATTN_Q_PRESCALED)     # forced two groups
+            assert torch.isfinite(one).all()
+            assert torch.equal(one, two), (scale_k, tdt)
+
+
 def test_attention_fp32_matches_reference():
     from daclip_amd import _lib
     B, L, H = 2, 256, 4

@@ -121,6 +121,24 @@ def test_loop_sde_step_pixel_kernel_bit_identical(unet_sd, monkeypatch, mode):
     assert torch.equal(px, planar)
 
 
+def test_unet_batch8_matches_single_image_fp16(unet_sd):
+    """At the bench's per-GPU batch (B = 8) several kernel choices differ from B = 1 (the 32x32
+    attention's query groups per wave, grid shapes); each image must still equal its
+    single-image run bit for bit (fp16, the headline dtype; sharding is bit-exact)."""
+    from daclip_amd import synth
+    from daclip_amd.unet import ConditionalUNet
+    m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype="fp16")
+    m.load_state_dict(unet_sd)
+    x = T(synth.synth_noise((8, 3, 256, 256), seed=95, tag="b8") * 0.3 + 0.5)
+    mu = T(synth.synth_images(8, 256, 256, seed=96))
+    tc = T(synth.synth_noise((8, 512), seed=97, tag="tc"))
+    ic = T(synth.synth_noise((8, 512), seed=98, tag="ic"))
+    full = m(x, mu, 42.0, text_context=tc, image_context=ic)
+    for i in (0, 5):
+        one = m(x[i:i + 1], mu[i:i + 1], 42.0, text_context=tc[i:i + 1], image_context=ic[i:i + 1])
+        assert torch.equal(one, full[i:i + 1]), i
+
+
 def test_unet_forward_256_fp32_vs_oracle(unets, unet_sd):
     from daclip_amd import synth
     from oracle import unet as OU
