@@ -70,7 +70,7 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
   if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0) {
     if (a.Cout <= 64) return conv3_rw_host(a, 128) > 0 ? 6 : 10;
     if (conv3_rw_host(a, 128) > 0)
-      return (long)(a.B * a.Ho * a.Wo / 128) * ((a.Cout + 127) / 128) >= 512 ? 7 : 11;
+      return (long)(a.Ho * a.Wo / 128) * ((a.Cout + 127) / 128) >= 64 ? 7 : 11;   // per image (batch-invariant)
   }
   if (v2ok) {
     if (kh == 1 && a.K <= BKE) return 8;

@@ -2179,7 +2179,10 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
       }
       if (conv3_rw(a, 128) > 0) {
         dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 127) / 128, 1);
-        if ((long)g.x * g.y >= 512)
+        // Chosen from ONE image's tile count (64 = the batch-8 grid's 512): the two forms walk
+        // the channels in different chunk orders (CK), so a batch-size-driven choice made an
+        // image's result depend on its batch (B = 16 vs 1 at the 32x32 level).
+        if ((long)(a.Ho * a.Wo / 128) * g.y >= 64)
           conv3_launch<T, 128, 128, 2, 2, 64>(a, g, conv3_rw(a, 128), st);
         else
           conv3_launch<T, 128, 128, 2, 4, 128>(a, g, conv3_rw(a, 128), st);

@@ -139,6 +139,27 @@ def test_unet_batch8_matches_single_image_fp16(unet_sd):
         assert torch.equal(one, full[i:i + 1]), i
 
 
+@pytest.mark.parametrize("dt", ["fp8", "fp16"])
+def test_unet_batch16_matches_single_image(unet_sd, dt):
+    """configs[4]'s per-GPU slice is 16 images (fp8 handles): each image equals its single-image
+    run bit for bit, so the 8-GPU sharding is exact there too. Grid-dependent kernel choices
+    must not change any output's arithmetic (the 32x32 v3 conv's channel-chunk form was once
+    chosen from the whole grid and differed between B = 16 and B = 1)."""
+    from daclip_amd import synth
+    from daclip_amd.unet import ConditionalUNet
+    m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype=dt)
+    m.load_state_dict(unet_sd)
+    x = T(synth.synth_noise((16, 3, 256, 256), seed=101, tag="b16") * 0.3 + 0.5)
+    mu = T(synth.synth_images(16, 256, 256, seed=102))
+    tc = T(synth.synth_noise((16, 512), seed=103, tag="tc"))
+    ic = T(synth.synth_noise((16, 512), seed=104, tag="ic"))
+    full = m(x, mu, 42.0, text_context=tc, image_context=ic)
+    assert torch.isfinite(full).all()
+    for i in (0, 11):
+        one = m(x[i:i + 1], mu[i:i + 1], 42.0, text_context=tc[i:i + 1], image_context=ic[i:i + 1])
+        assert torch.equal(one, full[i:i + 1]), i
+
+
 def test_unet_forward_256_fp32_vs_oracle(unets, unet_sd):
     from daclip_amd import synth
     from oracle import unet as OU
