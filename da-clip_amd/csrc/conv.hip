@@ -28,7 +28,8 @@ void conv_dispatch(const ConvArgs& a, hipStream_t st);
 // 2-stage, 20 = v4 with 32-pixel wave tiles 128x64, 21 = v5 weight-stationary 3x3 (64 -> 64),
 // 22 / 23 = conv_edge.hip init_conv (7x7, Cin 8, Cout 64) / final_conv (3x3, Cout <= 4),
 // 24 = conv_down.hip (4x4 stride-2 Downsample), 25 = v6 2-D halo 3x3 (conv3h_kernel), 26 = v4
-// row-phase upsample conv (ConvArgs::uph; labelled by the engine, not returned here).
+// row-phase upsample conv (ConvArgs::uph; labelled by the engine, not returned here), 27 = conv3r
+// register-stationary 3x3 (64 -> 64, conv3r.hip).
 int conv3_rw_host(const ConvArgs& a, int BM) {
   const int Wo = a.Wo, Ho = a.Ho;
   if (Wo <= 0 || (Wo & (Wo - 1))) return Wo % BM == 0 ? BM : 0;
@@ -60,6 +61,7 @@ int conv_variant(const ConvArgs& a, int kh, int elem_bytes) {
                   (g_conv3_force < 0 && g_conv3h_on == 1 && a.Cin >= 128 && !a.res1 && !a.res2 && !a.bbias)) &&
       conv3h_ok(a, elem_bytes))
     return 25;
+  if (kh == 3 && elem_bytes == 2 && (g_conv3_force < 0 || g_conv3_force == 70) && conv3r_ok(a)) return 27;
   if (kh == 3 && elem_bytes == 2 && (g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) return 21;
   if (kh == 3 && v2ok && !batched && epi_min && conv3_rw_host(a, 256) > 0 && g_conv3_force < 0) {
     const int RW = conv3_rw_host(a, 256);
@@ -144,7 +146,7 @@ bool conv_res_fusable(const ConvArgs& a) {
   if (g_conv3_force >= 0 || a.cwrap) return false;
   if ((a.ss && (a.ss_ld % 4 || a.Cout % 4 || ((uintptr_t)a.ss & 15))) || ((uintptr_t)a.bias & 15)) return false;
   const int v = conv_variant(a, 3, 2);
-  if (v == 12) return true;
+  if (v == 12 || v == 27) return true;            // v4 256x64 tiles, or conv3r (CIN 128)
   if (v != 20 && v != 7 && v != 11) return false;     // 128x64 v4 / v3 candidates only
   const bool kok = (a.C1 >= a.Cin || a.C1 % 32 == 0) && a.Cin % 32 == 0;
   return kok && conv3_rw_host(a, 128) > 0 && conv3_rw_host(a, 128) % 32 == 0;

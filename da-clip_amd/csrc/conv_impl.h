@@ -2082,6 +2082,10 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
       conv3h_launch<T>(a, st, g_conv3_force == 60 ? 0 : 1);
       return;
     }
+    if ((g_conv3_force < 0 || g_conv3_force == 70) && conv3r_ok(a)) {
+      conv3r<T>(a, st);
+      return;
+    }
     if ((g_conv3_force < 0 || (g_conv3_force >= 30 && g_conv3_force < 40)) && conv3w_ok(a)) {
       const int delay = g_conv3_force >= 30 ? (g_conv3_force - 30) * 2 : 6;   // swept: 4-10 best
       conv3w_launch<T>(a, delay, st);

@@ -129,6 +129,11 @@ inline bool conv3w_ok(const ConvArgs& a) {
 }
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
+// Register-stationary 3x3 conv, 64 -> 64 (conv3r.hip, 16-bit types): the shapes it serves
+// (DAC_CONV3R=0 turns it off) and its launcher.
+bool conv3r_ok(const ConvArgs& a);
+template <typename T>
+void conv3r(const ConvArgs& a, hipStream_t st);
 // init_conv (7x7, Cin 8 row-tap layout, Cout 64, bf16 / f16, plain or split-precision weights):
 // weight-stationary persistent kernel (conv_edge.hip).
 bool conv7_ok(const ConvArgs& a);

@@ -15,8 +15,15 @@ from typing import Optional, Sequence
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-# DAC_LIB_PATH: an alternative build of the same sources, for A/B measurements only.
-LIB_PATH = os.environ.get("DAC_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdaclip_hip.so")
+# DAC_LIB_PATH: an alternative build of the same sources, for A/B measurements only. A stale
+# value left in a shell would silently run another build, so setting it warns, and build_info()
+# (printed by smoke() and carried in every bench line) names the library actually loaded.
+DEFAULT_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdaclip_hip.so")
+LIB_PATH = os.environ.get("DAC_LIB_PATH") or DEFAULT_LIB_PATH
+if LIB_PATH != DEFAULT_LIB_PATH:
+    import warnings
+    warnings.warn(f"DAC_LIB_PATH is set: loading {LIB_PATH} instead of the in-tree {DEFAULT_LIB_PATH}",
+                  RuntimeWarning, stacklevel=2)
 
 DAC_F32, DAC_BF16, DAC_FP8, DAC_F16 = 0, 1, 2, 3
 DAC_SRC_F32, DAC_SRC_F16, DAC_SRC_BF16 = 0, 1, 2
@@ -162,10 +169,13 @@ def source_hash() -> str:
 
 
 def build_info() -> dict:
-    """{"build_id": the loaded library's id, "source_hash": this tree's, "matches": bool}."""
+    """{"build_id": the loaded library's id, "source_hash": this tree's, "matches": bool,
+    "lib_path": the file loaded, "lib_override": whether DAC_LIB_PATH chose it}."""
     bid = lib().dac_build_id().decode()
     src = source_hash()
-    return {"build_id": bid, "source_hash": src, "matches": bid.split(" ")[0] == src}
+    return {"build_id": bid, "source_hash": src, "matches": bid.split(" ")[0] == src,
+            "lib_path": os.path.relpath(LIB_PATH, os.path.dirname(os.path.dirname(os.path.dirname(
+                os.path.abspath(__file__))))), "lib_override": LIB_PATH != DEFAULT_LIB_PATH}
 
 
 def exports_present(names: Sequence[str] = EXPORTS):

@@ -295,3 +295,104 @@ def vision_keys(prefix: str, v: VisionConfig, control: bool) -> List[str]:
     sd: "OrderedDict[str, Shape]" = OrderedDict()
     _vit_tower(prefix, v, sd, control)
     return list(sd)
+
+
+# ----------------------------------------------------------------------------- reference FLOPs
+# The work the REFERENCE defines per forward, counted as torch.utils.flop_counter does on the
+# reference's CPU path: 2*MAC over conv2d (2 x out elements x Cin x kh x kw),
+# addmm / mm / bmm / einsum; nothing for norms, softmax, activations or elementwise ops, and —
+# on the CPU path — nothing for the ViT's nn.MultiheadAttention core, which runs as the CPU
+# flash SDPA kernel the counter has no formula for. These reproduce §8(d)'s constants from the
+# shapes alone: 266.172 GF per UNet step at 256^2 (1129.09 at 512^2, Wild-IR 348.88 at 512^2),
+# 18.159 GF per ViT-B/32 encode_image(control=True) (324.0 for ViT-L/14): 26.635 TF per
+# restored 256^2 image at T = 100. The engine's own count (dac_unet_flops / dac_encode_flops)
+# is the EXECUTED work, lower by the exact shortcuts it takes (one-key attn2 collapse, the
+# LinearAttention re-association, row-phase upsample convs) and higher by the ViT attention.
+
+def _conv(h: int, w: int, cin: int, cout: int, k: int) -> float:
+    return 2.0 * h * w * cout * cin * k * k
+
+
+def _ref_resblock(h, w, din, dout, td):
+    # module_util.py:132-153: mlp Linear(td, 2 dout) on [1, td], two 3x3 convs, 1x1 res_conv
+    f = 2.0 * td * 2 * dout + _conv(h, w, din, dout, 3) + _conv(h, w, dout, dout, 3)
+    return f + (_conv(h, w, din, dout, 1) if din != dout else 0.0)
+
+
+def _ref_linear_attention(h, w, c):
+    # module_util.py:157-185: to_qkv 1x1 (c -> 384), two einsums over 4 heads x 32 x 32 x n,
+    # to_out 1x1 (128 -> c)
+    n = h * w
+    return _conv(h, w, c, 384, 1) + 2 * (2.0 * 4 * 32 * 32 * n) + _conv(h, w, 128, c, 1)
+
+
+def _ref_spatial_transformer(h, w, c, ctx):
+    # attention.py:152-261 with one context token: proj_in / proj_out 1x1; attn1 q, k, v (mm),
+    # q k^T and attn v (bmm, L^2 C each), to_out (addmm); attn2 to_q (mm), to_k / to_v on the
+    # single context row, q k^T over that one key (a bmm of 2 L C; the attn x v einsum contracts
+    # over j = 1, which torch.einsum evaluates as a broadcast multiply, not a bmm), to_out;
+    # GEGLU proj (C -> 8C) and ff out (4C -> C)
+    L = h * w
+    f = 2 * _conv(h, w, c, c, 1)
+    f += 3 * 2.0 * L * c * c + 2 * 2.0 * L * L * c + 2.0 * L * c * c
+    f += 2.0 * L * c * c + 2 * 2.0 * ctx * c + 2.0 * L * c + 2.0 * L * c * c
+    f += 2.0 * L * c * 8 * c + 2.0 * L * 4 * c * c
+    return f
+
+
+def reference_unet_flops(cfg: UNetConfig, H: int, W: int) -> float:
+    """FLOPs of one ConditionalUNet.forward on one image (DenoisingUNet_arch.py:118-174; the
+    Wild-IR variant's scale-0.5 down / up convs, config/wild-ir/.../DenoisingUNet_arch.py)."""
+    s = 2 ** cfg.depth
+    H, W = H + (s - H % s) % s, W + (s - W % s) % s           # check_image_size (reflect pad)
+    nf, td = cfg.nf, cfg.time_dim
+    f = _conv(H, W, 2 * cfg.in_nc, nf, 7)
+    h, w = H, W
+    if cfg.scale == 0.5:
+        h, w = H // 2, W // 2
+        f += _conv(h, w, nf, nf, 4)
+    f += 2.0 * nf * td + 2.0 * td * td                         # time_mlp on the [1] time tensor
+    if cfg.context_dim > 0 and cfg.use_degra_context:
+        f += 2.0 * cfg.context_dim * td + 2.0 * td * td + 2.0 * td * td
+    attn = lambda hh, ww, c, lvl: (_ref_spatial_transformer(hh, ww, c, cfg.context_dim)
+                                   if cfg.uses_transformer(lvl) else _ref_linear_attention(hh, ww, c))
+    levels = cfg.levels()
+    for i, (din, dout) in enumerate(levels):
+        f += 2 * _ref_resblock(h, w, din, din, td) + attn(h, w, din, i)
+        if i != cfg.depth - 1:
+            f += _conv(h // 2, w // 2, din, dout, 4)
+            h, w = h // 2, w // 2
+        else:
+            f += _conv(h, w, din, dout, 3)
+    mid = levels[-1][1]
+    f += 2 * _ref_resblock(h, w, mid, mid, td)
+    f += (_ref_spatial_transformer(h, w, mid, cfg.context_dim) if cfg.use_image_context and cfg.context_dim > 0
+          else _ref_linear_attention(h, w, mid))
+    for i in reversed(range(cfg.depth)):
+        din, dout = levels[i]
+        f += 2 * _ref_resblock(h, w, dout + din, dout, td) + attn(h, w, dout, i)
+        if i != 0:
+            h, w = 2 * h, 2 * w
+        f += _conv(h, w, dout, din, 3)
+    if cfg.scale == 0.5:
+        h, w = 2 * h, 2 * w
+        f += _conv(h, w, nf, nf, 3)
+    f += _ref_resblock(h, w, 2 * nf, nf, td) + _conv(h, w, nf, cfg.out_nc, 3)
+    return f
+
+
+def reference_encode_flops(v: VisionConfig = VIT_B_32) -> float:
+    """FLOPs of DaCLIP.encode_image(image, control=True) on one image (daclip_model.py:46-53):
+    the controller tower (+ its 12 / 24 zero-module linears) and the CLIP tower, each a patch conv,
+    `layers` ResidualAttentionBlocks (in_proj, out_proj, MLP) and the head projection."""
+    L, wd = v.tokens, v.width
+    hid = int(wd * v.mlp_ratio)
+    tower = _conv(v.grid, v.grid, 3, wd, v.patch_size)
+    tower += v.layers * (2.0 * L * wd * 3 * wd + 2.0 * L * wd * wd + 2 * 2.0 * L * wd * hid)
+    tower += 2.0 * wd * v.embed_dim
+    return 2 * tower + v.layers * 2.0 * L * wd * wd
+
+
+def reference_tflop_per_image(cfg: UNetConfig, vision: VisionConfig, H: int, W: int, T: int) -> float:
+    """T x F_unet(H, W) + F_clip, in TFLOP per restored image."""
+    return (T * reference_unet_flops(cfg, H, W) + reference_encode_flops(vision)) / 1e12

@@ -65,3 +65,23 @@ def test_build_id_matches_sources():
         pytest.skip("libdaclip_hip.so not built")
     info = _lib.build_info()
     assert info["matches"], info
+
+
+def test_host_asan_argument_validation():
+    """the C ABI's argument-validation paths under a host AddressSanitizer build
+    (tools/abi_asan.cpp, `make -C da-clip_amd asan`: capi.cpp / engine.cpp with -fsanitize=address
+    on the host side). Null handles and pointers, bad dtypes / configs and (on a GPU box) a
+    handle driven through set_weight / forward-before-finalize / strict-load errors must return
+    their DAC_E* codes with no heap error or leak."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "abi_asan")
+    if not os.path.exists(exe):
+        r = subprocess.run(["make", "-C", os.path.join(ROOT, "da-clip_amd"), "-j8", "asan"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            pytest.skip("host ASan build unavailable: " + r.stderr[-300:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-2000:]
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    assert "all checks passed" in r.stdout

@@ -23,3 +23,16 @@ def test_daclip_spec_b32():
     ours = arch.daclip_state_spec(arch.VIT_B_32, arch.TEXT_B_32)
     assert sorted(ours.items()) == sorted(_ref("daclip_b32"))
     assert len(ours) == 631
+
+
+def test_reference_flop_model_reproduces_survey_constants():
+    """the reference's work per step / encode, from shapes (torch flop_counter
+    convention on the reference's CPU path), to the precision the survey quotes."""
+    from daclip_amd import arch
+    gf = lambda f: f / 1e9
+    assert round(gf(arch.reference_unet_flops(arch.UNetConfig(), 256, 256)), 3) == 266.172
+    assert round(gf(arch.reference_unet_flops(arch.UNetConfig(), 512, 512)), 2) == 1129.09
+    assert round(gf(arch.reference_unet_flops(arch.WILD_IR_UNET, 512, 512)), 2) == 348.88
+    assert round(gf(arch.reference_encode_flops(arch.VIT_B_32)), 3) == 18.159
+    assert round(gf(arch.reference_encode_flops(arch.VIT_L_14)), 1) == 324.0
+    assert round(arch.reference_tflop_per_image(arch.UNetConfig(), arch.VIT_B_32, 256, 256, 100), 3) == 26.635

@@ -33,8 +33,10 @@ def _run(qkv, B, L, H, dtype, variant):
 
 
 # (B, L, H): L = 1024 with 16 heads (mid / up levels, 4 query groups per wave) and 8 heads
-# (down level, 2 groups), a 256-token and a 128-token case, and ragged L (fallback kernel).
-CASES = [(8, 1024, 16), (8, 1024, 8), (2, 256, 4), (1, 128, 2), (3, 100, 2)]
+# (down level, 2 groups), a 256-token and a 128-token case, ragged L (fallback kernel), and
+# L = 4096 (the 64x64-token SpatialTransformer of a 512^2 UIR restore: the staged-tile kernel the
+# engine takes for L > 1024, here also with the prescaled q the 16-bit engine emits).
+CASES = [(8, 1024, 16), (8, 1024, 8), (2, 256, 4), (1, 128, 2), (3, 100, 2), (2, 4096, 8)]
 
 
 @pytest.mark.parametrize("B,L,H", CASES)

@@ -5,9 +5,10 @@ kernel choice on random inputs and compares the full output with a naive one-thr
 fp32 conv of the same bf16 operands and the same epilogue (bias, per-image scale/shift, SiLU,
 residual): max |diff| / max |ref| < 1e-2; and, independently of any GPU code, 2048 sampled
 outputs per shape against a host fp64 recomputation from the operands copied back ("host rel",
-same bound). Choices: -1 built-in (v5 weight-stationary for
-64 -> 64, swapped-epilogue v4 elsewhere), 18 v4 LDS epilogue, 40 / 41 swapped v4 256x64 /
-128x64, 20 v4 128x64, 30 v5 without the SIMD-partner offset, 0 v3."""
+same bound). Choices: -1 built-in (conv3r register-stationary for 64 -> 64 on 256-pixel rows, v5
+weight-stationary for 64 -> 64 on 128-pixel rows, swapped-epilogue v4 elsewhere), 70 conv3r, 18 v4
+LDS epilogue, 40 / 41 swapped v4 256x64 / 128x64, 20 v4 128x64, 30 v5 without the SIMD-partner
+offset, 0 v3."""
 import os
 import re
 import subprocess
@@ -21,15 +22,17 @@ BIN = os.path.join(ROOT, "tools", "convbench")
 @pytest.mark.gpu
 def test_conv3x3_kernels_match_naive_reference():
     assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
-    out = subprocess.run([BIN, "1", "3x3", "check", "-1,18,40,41,20,30,0"], capture_output=True,
+    out = subprocess.run([BIN, "1", "3x3", "check", "-1,70,18,40,41,20,30,0"], capture_output=True,
                          text=True, timeout=120, cwd=ROOT)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check rel" in l]
     bad = [l for l in rows if not l.rstrip().endswith("OK")]
     assert len(rows) >= 40 and not bad, "\n".join(bad) or out.stdout[-2000:]
-    # The shapes that take the v5 kernel by default really ran it (variant 21).
+    # The shapes that take conv3r (variant 27: the three 256-wide 64 -> 64 shapes) and v5
+    # (variant 21: the 128-wide one) by default really ran them.
+    c3r = [l for l in rows if re.search(r"64->64 .*f-1\s+variant 27", l)]
     v5 = [l for l in rows if re.search(r"64->64 .*f-1\s+variant 21", l)]
-    assert len(v5) == 4, "\n".join(rows)
+    assert len(c3r) == 3 and len(v5) == 1, "\n".join(rows)
 
 
 @pytest.mark.gpu

@@ -102,8 +102,19 @@ def test_headline_fp32_matches_reference(headline, unet_sd):
     check("headline_fp32", g, ic, dc, out, ctx_tol=1e-4, out_tol=1e-3, unsat_tol=1e-2)
 
 
+def test_headline_fp16_matches_reference(headline, unet_sd):
+    """fp16, the bench's headline dtype (bench.py --dtype fp16, the default): the 1e-3 dB bar,
+    every copy identical, and float bounds at least as tight as bf16's (fp16's significand is 8x
+    finer; the encoder contexts carry fp16 activation rounding)."""
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    g, lq, n0, steps = headline
+    ic, dc, out = restore("fp16", g, lq, n0, steps, unet_sd)
+    check("headline_fp16", g, ic, dc, out, ctx_tol=5e-3, out_tol=8e-4, unsat_tol=0.1)
+    assert calculate_psnr(tensor2img(torch.from_numpy(out[0])), g["out_u8"]) > 50.0
+
+
 def test_headline_bf16_matches_reference(headline, unet_sd):
-    """The benchmarked mode. Measured: dPSNR 2.9e-4 dB, 55.9 dB against the reference's uint8
+    """BASELINE configs[1]'s dtype (measured under the bench's `modes`). Measured: dPSNR 2.9e-4 dB, 55.9 dB against the reference's uint8
     output, float max-rel 3.2e-4 (bf16 weights with sum-keeping rounding; split-precision
     init_conv / final_conv / final_res_block.res_conv, engine.cpp)."""
     from daclip_amd.preprocess import tensor2img, calculate_psnr

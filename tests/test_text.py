@@ -58,10 +58,10 @@ def test_tokenizer_needs_vocab(monkeypatch):
 
 # ------------------------------------------------------------------ GPU: HIP path
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
 def test_encode_text_matches_reference(golden, dt):
     from daclip_amd.open_clip import DaCLIP
-    tol = 1e-4 if dt == "fp32" else 5e-2
+    tol = {"fp32": 1e-4, "bf16": 5e-2, "fp16": 1e-2}[dt]
     g = golden("text_small.npz")
     m = DaCLIP(arch.VisionConfig(**SMALL_V), arch.TextConfig(**SMALL_T), dtype=dt)
     m.load_synthetic(0)
@@ -90,12 +90,17 @@ def test_degradation_argmax_bit_exact(golden):
     assert np.array_equal(am.cpu().numpy(), g["argmax"])
     assert np.array_equal(np.argsort(-probs, 1)[:, :3], np.argsort(-g["probs"], 1)[:, :3])
     assert np.abs(probs - g["probs"]).max() < 1e-4
-    # bf16 (perf) path: same classes.
-    mb = DaCLIP(dtype="bf16")
-    mb.load_synthetic(0)
-    _, dcb = mb.encode_image(torch.from_numpy(text_images()).cuda(), control=True)
-    _, amb = mb.degradation_probs(dcb, mb.encode_text(torch.from_numpy(g["tokens"])))
-    assert np.array_equal(amb.cpu().numpy(), g["argmax"])
+    # 16-bit (perf) paths: the same classes (the north star's bit-exact argmax) — fp16 is the
+    # bench's headline dtype, bf16 the dtype BASELINE configs[1] names. (The top-3 ranking is a
+    # parity-mode property: two of these images have runner-up classes within 16-bit rounding.)
+    for dt in ("fp16", "bf16"):
+        mb = DaCLIP(dtype=dt)
+        mb.load_synthetic(0)
+        _, dcb = mb.encode_image(torch.from_numpy(text_images()).cuda(), control=True)
+        pb, amb = mb.degradation_probs(dcb, mb.encode_text(torch.from_numpy(g["tokens"])))
+        print(f"argmax {dt}: max |dprob| {np.abs(pb.cpu().numpy() - g['probs']).max():.3e}")
+        assert np.array_equal(amb.cpu().numpy(), g["argmax"]), dt
+        assert np.abs(pb.cpu().numpy() - g["probs"]).max() < (5e-3 if dt == "fp16" else 5e-2), dt
 
 
 @pytest.mark.gpu

@@ -52,24 +52,30 @@ def wild_unets():
     from daclip_amd.unet import ConditionalUNet
     sd = synth.synth_state_dict(arch.unet_state_spec(arch.WILD_IR_UNET), 0)
     out = {}
-    for dt in ("fp32", "bf16"):
+    for dt in ("fp32", "bf16", "fp16"):
         m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 768, False, True, scale=0.5, dtype=dt)
         m.load_state_dict(sd)
         out[dt] = m
     return out
 
 
+# Bars: fp32 exact-f32 MFMA; bf16 / fp16 storage with fp32 accumulation (fp16's 11-bit
+# significand is 8x finer than bf16's: the bench's Wild-IR line runs fp16).
+TOL = {"fp32": 1e-4, "bf16": 5e-2, "fp16": 1e-2}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
 def test_wild_unet_matches_reference(golden, wild_unets, dt):
     g = golden("wild_unet_fwd.npz")
-    tol = 1e-4 if dt == "fp32" else 5e-2
     for tag in ("32x32", "48x40"):
         T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
         out = wild_unets[dt](T(g[tag + "_xt"]), T(g[tag + "_mu"]), 37.0,
                              image_context=T(g[tag + "_ic"])).cpu().numpy()
         assert out.shape == g[tag + "_out"].shape
-        assert rel(out, g[tag + "_out"]) < tol
+        r = rel(out, g[tag + "_out"])
+        print(f"wild unet {dt} {tag}: rel {r:.3e}")
+        assert r < TOL[dt]
 
 
 @pytest.mark.gpu
@@ -93,13 +99,13 @@ def test_wild_loop_512_batch_invariant(wild_unets):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
 def test_l14_encode_matches_reference(golden, dt):
     from daclip_amd.open_clip import DaCLIP
     m = DaCLIP(arch.VIT_L_14, arch.TEXT_L_14, dtype=dt, with_text=False)
     m.load_synthetic(0)
     ic, dc = m.encode_image(torch.from_numpy(wild_images()).cuda(), control=True)
     g = golden("wild_l14_encode.npz")
-    tol = 1e-4 if dt == "fp32" else 5e-2
-    assert rel(ic.cpu().numpy(), g["image_context"]) < tol
-    assert rel(dc.cpu().numpy(), g["degra_context"]) < tol
+    ri, rd = rel(ic.cpu().numpy(), g["image_context"]), rel(dc.cpu().numpy(), g["degra_context"])
+    print(f"l14 encode {dt}: rel image {ri:.3e} degra {rd:.3e}")
+    assert ri < TOL[dt] and rd < TOL[dt]

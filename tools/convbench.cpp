@@ -16,6 +16,7 @@
 using namespace dac;
 extern "C" void dac_conv3_force(int v);
 extern "C" void dac_conv2_force(int v);
+extern "C" void dac_conv3r_enable(int on);
 typedef __bf16 bf16;
 
 struct Shape { const char* name; int B, H, W, cin, cout, kh, s, p, up, act, ss, res, kwp = 0, bias = 0; };
@@ -792,7 +793,118 @@ static int uph_check(int iters) {
   return fails;
 }
 
+
+// ---- conv3r (conv3r.hip) check: two-source inputs (torch.cat of x1 | x2 with different pitches),
+// the fused 1x1 res_conv output y2, residual / scale-shift / SiLU epilogues, against a host fp64
+// recomputation at sampled outputs; timed against the kernel the dispatcher takes without it.
+static int c3r_check(int iters) {
+  struct Q { const char* name; int B, H, W, c1, c2, ld2, act, ss, res, fuse; };
+  const Q shapes[] = {
+    {"c3r 64->64 ss+silu", 2, 256, 256, 64, 0, 0, 1, 1, 0, 0},
+    {"c3r 64->64 silu+res", 2, 256, 256, 64, 0, 0, 1, 0, 1, 0},
+    {"c3r 64->64 plain 256x512", 1, 256, 512, 64, 0, 0, 0, 0, 0, 0},
+    {"c3r 64|64->64 ss+silu +1x1", 2, 256, 256, 64, 64, 96, 1, 1, 0, 1},
+    {"c3r 128->64 silu +1x1 256x512", 1, 256, 512, 128, 0, 0, 1, 0, 0, 1},
+    {"c3r 128->64 ss+silu", 2, 256, 256, 128, 0, 0, 1, 1, 0, 0},
+    {"c3r 64|64->64 ss+silu +1x1 B8", 8, 256, 256, 64, 64, 64, 1, 1, 0, 1},
+  };
+  int bad = 0;
+  for (const Q& q : shapes) {
+    const int cin = q.c1 + q.c2, ld1 = q.c1, ld2 = q.c2 ? q.ld2 : 0;
+    const size_t npx = (size_t)q.B * q.H * q.W;
+    const size_t nw = (size_t)64 * 9 * cin, nw2 = (size_t)64 * cin;
+    bf16 *x1, *x2 = nullptr, *w, *w2, *y, *y2, *res;
+    float *ss, *bias;
+    CK(hipMalloc(&x1, npx * ld1 * 2)); if (q.c2) CK(hipMalloc(&x2, npx * ld2 * 2));
+    CK(hipMalloc(&w, nw * 2)); CK(hipMalloc(&w2, nw2 * 2)); CK(hipMalloc(&y, npx * 64 * 2));
+    CK(hipMalloc(&y2, npx * 64 * 2)); CK(hipMalloc(&res, npx * 64 * 2));
+    CK(hipMalloc(&ss, q.B * 128 * 4)); CK(hipMalloc(&bias, 64 * 4));
+    fill_rand<<<(npx * ld1 + 255) / 256, 256>>>(x1, npx * ld1, 11, 2.f);
+    if (q.c2) fill_rand<<<(npx * ld2 + 255) / 256, 256>>>(x2, npx * ld2, 12, 2.f);
+    fill_rand<<<(nw + 255) / 256, 256>>>(w, nw, 13, 0.1f);
+    fill_rand<<<(nw2 + 255) / 256, 256>>>(w2, nw2, 14, 0.2f);
+    fill_rand<<<(npx * 64 + 255) / 256, 256>>>(res, npx * 64, 15, 2.f);
+    fill_rand_f<<<1, 256>>>(ss, q.B * 128, 16, 1.f);
+    fill_rand_f<<<1, 64>>>(bias, 64, 17, 1.f);
+    void* zero; CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+    ConvArgs a{};
+    a.x1 = x1; a.ld1 = ld1; a.C1 = q.c1; a.x2 = x2; a.ld2 = ld2; a.Cin = cin; a.Hs = q.H; a.Ws = q.W;
+    a.B = q.B; a.Ho = q.H; a.Wo = q.W; a.Cout = 64; a.K = 9 * cin; a.w = w; a.y = y; a.ldy = 64;
+    a.act = q.act; a.bias = bias; a.zero = zero;
+    if (q.ss) { a.ss = ss; a.ss_ld = 128; }
+    if (q.res) { a.res1 = res; a.ldr1 = 64; }
+    if (q.fuse) { a.w2 = w2; a.y2 = y2; a.ldy2 = 64; }
+    double t[2] = {0, 0};
+    std::vector<bf16> hy(npx * 64), hy2(q.fuse ? npx * 64 : 0);
+    for (int arm = 1; arm >= 0; --arm) {                     // 1: conv3r, 0: without it
+      dac_conv3r_enable(arm);
+      dac_conv3_force(-1);
+      if (q.fuse && !conv_res_fusable(a)) { printf("%-32s arm %d: no fused kernel\n", q.name, arm); continue; }
+      conv<bf16>(a, 3, 3, 1, 1, 0);
+      CK(hipDeviceSynchronize());
+      if (arm == 1) {
+        printf("%-32s variant %d", q.name, conv_variant(a, 3, 2));
+        CK(hipMemcpy(hy.data(), y, npx * 64 * 2, hipMemcpyDeviceToHost));
+        if (q.fuse) CK(hipMemcpy(hy2.data(), y2, npx * 64 * 2, hipMemcpyDeviceToHost));
+      }
+      hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) conv<bf16>(a, 3, 3, 1, 1, 0);
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      t[arm] = ms * 1e3 / iters;
+    }
+    dac_conv3r_enable(1);
+    // Host fp64 reference at sampled outputs.
+    std::vector<bf16> hx1(npx * ld1), hx2(q.c2 ? npx * ld2 : 0), hw(nw), hw2(nw2), hr(npx * 64);
+    std::vector<float> hss(q.B * 128), hb(64);
+    CK(hipMemcpy(hx1.data(), x1, hx1.size() * 2, hipMemcpyDeviceToHost));
+    if (q.c2) CK(hipMemcpy(hx2.data(), x2, hx2.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hw.data(), w, nw * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hw2.data(), w2, nw2 * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hr.data(), res, hr.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hss.data(), ss, hss.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hb.data(), bias, 256, hipMemcpyDeviceToHost));
+    auto xin = [&](size_t pix, int c) -> double {
+      return c < q.c1 ? bf2f(hx1[pix * ld1 + c]) : bf2f(hx2[pix * ld2 + c - q.c1]);
+    };
+    double d1 = 0, m1 = 0, d2 = 0, m2 = 0;
+    uint32_t st = 777u;
+    for (int k = 0; k < 4096; ++k) {
+      st = st * 1664525u + 1013904223u;
+      const size_t i = ((size_t)st * 2654435761u) % (npx * 64);
+      const int n = (int)(i % 64);
+      const size_t m = i / 64;
+      const int b = (int)(m / ((size_t)q.H * q.W)), rr = (int)(m % ((size_t)q.H * q.W)), oh = rr / q.W, ow = rr % q.W;
+      double acc = 0, acc2 = 0;
+      for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx) {
+          const int ih = oh - 1 + ky, iw = ow - 1 + kx;
+          if (ih < 0 || iw < 0 || ih >= q.H || iw >= q.W) continue;
+          const size_t pix = ((size_t)b * q.H + ih) * q.W + iw;
+          for (int c = 0; c < cin; ++c) acc += xin(pix, c) * bf2f(hw[((size_t)n * 9 + ky * 3 + kx) * cin + c]);
+        }
+      for (int c = 0; c < cin; ++c) acc2 += xin(m, c) * bf2f(hw2[(size_t)n * cin + c]);
+      acc += hb[n];
+      if (q.ss) acc = acc * (hss[b * 128 + n] + 1.0) + hss[b * 128 + 64 + n];
+      if (q.act == 1) acc = acc / (1.0 + std::exp(-acc));
+      if (q.res) acc += bf2f(hr[m * 64 + n]);
+      d1 = fmax(d1, fabs((double)bf2f(hy[m * 64 + n]) - acc)); m1 = fmax(m1, fabs(acc));
+      if (q.fuse) { d2 = fmax(d2, fabs((double)bf2f(hy2[m * 64 + n]) - acc2)); m2 = fmax(m2, fabs(acc2)); }
+    }
+    const bool ok = d1 / m1 < 1e-2 && (!q.fuse || d2 / m2 < 1e-2);
+    bad += !ok;
+    printf("  conv3r %7.1f us, without %7.1f us  host rel %.2e", t[1], t[0], d1 / m1);
+    if (q.fuse) printf(" y2 rel %.2e", d2 / m2);
+    printf("  check %s\n", ok ? "OK" : "FAIL");
+    hipFree(x1); if (x2) hipFree(x2); hipFree(w); hipFree(w2); hipFree(y); hipFree(y2); hipFree(res);
+    hipFree(ss); hipFree(bias); hipFree(zero);
+  }
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "c3r")) return c3r_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
   if (argc > 1 && !strcmp(argv[1], "uph")) return uph_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "q8")) return q8_check(argc > 2 ? atoi(argv[2]) : 20);
