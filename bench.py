@@ -45,6 +45,10 @@ for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
     KERNEL_SYMBOL[(321, _dt)] = f"_ZN3dac13conv3w_kernelI{_m}Li8ELi4ELi2EEEvNS_8ConvArgsEii"
     KERNEL_SYMBOL[(306, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
     KERNEL_SYMBOL[(307, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
+    # class 327 = conv3r (conv3r.hip: register-stationary 3x3, CIN 64 / 128, epilogue variants)
+    KERNEL_SYMBOL[(327, _dt)] = tuple(
+        f"_ZN3dac13conv3r_kernelI{_m}Li{cin}ELb{res}ELb{silu}ELb{fuse}EEEvNS_8ConvArgsEi"
+        for cin in (64, 128) for res in (0, 1) for silu in (0, 1) for fuse in (0, 1))
 # fp8 handles: class 340 = conv3q (e4m3 64 -> 64 ResBlock block2 on the block-scaled MFMA).
 KERNEL_SYMBOL[(340, "fp8")] = "_ZN3dac13conv3q_kernelIDF16bEEvNS_8ConvArgsEPKhS3_ii"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -99,15 +103,14 @@ def parse():
                         "fp16 (equal-batch comparison for fp8), fp32 = the parity mode on the main workload; "
                         "'none' to skip")
     p.add_argument("--kernel-id", type=int, default=None,
-                   help="conv class timed for the roofline (kh*100 + variant; default 312 = 3x3 "
-                        "interleaved-row v4 tiles, 340 = conv3q, the e4m3 ResBlock block2 kernel, for --dtype fp8)")
+                   help="conv class timed for the roofline (kh*100 + variant, e.g. 312 = 3x3 interleaved-row "
+                        "v4 tiles, 327 = conv3r, 340 = conv3q); default: the class with the largest total time "
+                        "in one eager restore")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the PSNR-vs-reference sample")
     p.add_argument("--cpu-steps", type=int, default=5, help="UNet steps in the CPU sample (>= 5)")
     a = p.parse_args()
-    if a.kernel_id is None:
-        a.kernel_id = 340 if a.dtype == "fp8" else 312
     wild = a.model == "wild-ir"
     a.batch = a.batch or (2 if wild else 8)
     a.res = a.res or (512 if wild else 256)
@@ -387,22 +390,27 @@ def roofline_entry(kernel_id, dtype, n, mean_ms, fl, by, eager_ms, graph_ms, pmc
 
 
 # Conv classes a line's dominant-kernel search times (kh*100 + conv_variant; engine.cpp conv_call).
-ROOF_CANDIDATES = (312, 321, 326, 307, 311, 306, 310, 320, 324, 322, 323, 340, 115, 116, 117, 118, 108)
+ROOF_CANDIDATES = (327, 312, 321, 326, 307, 311, 306, 310, 320, 324, 322, 323, 340, 115, 116, 117, 118, 108)
 
 
-def dominant_roofline(h, step, dtype, graph_ms):
-    """Roofline of the conv class with the largest total time in one eager restore."""
-    best = None
+def dominant_roofline(h, step, dtype, graph_ms, pmc_ok=False):
+    """Roofline of the conv class with the largest total time in one eager restore (each class
+    timed by its own eager replay), plus every timed class's share (`classes`)."""
+    rows = []
     for k in ROOF_CANDIDATES:
         n, mean_ms, fl, by, eager_ms = profile_class(h, step, k)
-        if n > 0 and (best is None or n * mean_ms > best[1] * best[2]):
-            best = (k, n, mean_ms, fl, by, eager_ms)
-    if best is None:
+        if n > 0:
+            rows.append((n * mean_ms, k, n, mean_ms, fl, by, eager_ms))
+    if not rows:
         return None
-    k, n, mean_ms, fl, by, eager_ms = best
-    r = roofline_entry(k, dtype, n, mean_ms, fl, by, eager_ms, graph_ms)
+    rows.sort(reverse=True)
+    _, k, n, mean_ms, fl, by, eager_ms = rows[0]
+    r = roofline_entry(k, dtype, n, mean_ms, fl, by, eager_ms, graph_ms, pmc_entry(k, dtype) if pmc_ok else None)
     r["class_ms_per_restore"] = round(n * mean_ms, 3)
     r["selection"] = "conv class with the largest eager total over " + ",".join(map(str, ROOF_CANDIDATES))
+    r["classes"] = [{"class": kk, "launches": nn, "ms_per_restore": round(nn * mm, 3),
+                     "frac_of_peak": round(ff / (mm * 1e-3) / 1e12 / MFMA_PEAK[dtype], 4)}
+                    for _, kk, nn, mm, ff, _, _ in rows]
     return r
 
 
@@ -498,9 +506,18 @@ def main():
         # fp16 storage saturates at 65504: a non-finite restore is an error, never a number.
         raise SystemExit(f"bench: non-finite restored outputs in {args.dtype} mode")
     n_launch, mean_ms, fl, by, eager_ms = 0, 0.0, 0.0, 0.0, 0.0
+    roof = None
+    # The committed PMC passes were collected on the default workload only.
+    default_wl = args.model == "universal-ir" and args.batch == 8 and args.res == 256
     if not args.no_roofline:
         # Roofline of the dominant kernel class (HIP events per launch on the kernel's stream).
-        n_launch, mean_ms, fl, by, eager_ms = profile_class(h, step, args.kernel_id)
+        if args.kernel_id is None:
+            roof = dominant_roofline(h, step, args.dtype, el / args.steps * 1e3, pmc_ok=default_wl)
+        else:
+            n_launch, mean_ms, fl, by, eager_ms = profile_class(h, step, args.kernel_id)
+            if n_launch > 0:
+                roof = roofline_entry(args.kernel_id, args.dtype, n_launch, mean_ms, fl, by, eager_ms,
+                                      el / args.steps * 1e3, pmc_entry(args.kernel_id, args.dtype) if default_wl else None)
 
     psnr = None
     if rank == 0 and not args.no_psnr:
@@ -511,13 +528,6 @@ def main():
 
     if rank == 0:
         images = n_glob * args.steps
-        roof = None
-        # The committed PMC passes were collected on the default workload only.
-        default_wl = args.model == "universal-ir" and args.batch == 8 and args.res == 256
-        pmc = pmc_entry(args.kernel_id, args.dtype) if default_wl else None
-        if n_launch > 0:
-            roof = roofline_entry(args.kernel_id, args.dtype, n_launch, mean_ms, fl, by, eager_ms,
-                                  el / args.steps * 1e3, pmc)
         uflops = unet.flops(B, R, R)
         eflops = clip.flops(B)
         total_tf = (args.T * uflops + eflops) / B / 1e12
