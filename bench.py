@@ -49,6 +49,8 @@ for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
     KERNEL_SYMBOL[(327, _dt)] = tuple(
         f"_ZN3dac13conv3r_kernelI{_m}Li{cin}ELb{res}ELb{silu}ELb{fuse}EEEvNS_8ConvArgsEi"
         for cin in (64, 128) for res in (0, 1) for silu in (0, 1) for fuse in (0, 1))
+    # class 350 = the fused ResBlock (rbfuse.hip: block1 + block2 (+ res_conv) in one launch)
+    KERNEL_SYMBOL[(350, _dt)] = tuple(f"_ZN3dac13rbfuse_kernelI{_m}Li{cin}EEEvNS_6RbArgsEi" for cin in (64, 128))
 # fp8 handles: class 340 = conv3q (e4m3 64 -> 64 ResBlock block2 on the block-scaled MFMA).
 KERNEL_SYMBOL[(340, "fp8")] = "_ZN3dac13conv3q_kernelIDF16bEEvNS_8ConvArgsEPKhS3_ii"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -390,7 +392,7 @@ def roofline_entry(kernel_id, dtype, n, mean_ms, fl, by, eager_ms, graph_ms, pmc
 
 
 # Conv classes a line's dominant-kernel search times (kh*100 + conv_variant; engine.cpp conv_call).
-ROOF_CANDIDATES = (327, 312, 321, 326, 307, 311, 306, 310, 320, 324, 322, 323, 340, 115, 116, 117, 118, 108)
+ROOF_CANDIDATES = (350, 327, 312, 321, 326, 307, 311, 306, 310, 320, 324, 322, 323, 340, 115, 116, 117, 118, 108)
 
 
 def dominant_roofline(h, step, dtype, graph_ms, pmc_ok=False):

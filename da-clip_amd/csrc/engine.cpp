@@ -1016,6 +1016,52 @@ struct UNetNet {
   const void* resblock(Run& r, const RB& rb, const void* xa, int Ca, const void* xb, int Cb,
                        int B, int H, int W, const float* ss) {
     const size_t M = (size_t)B * H * W;
+    if constexpr (sizeof(T) == 2) {
+      // The whole ResBlock as one launch (rbfuse.hip) where it applies: h and the res_conv output
+      // stay in LDS. (fp8 handles keep their e4m3 pair below.)
+      const bool q8pair = rb.c2.q8w && q8_on();
+      RbArgs ra{};
+      ra.x1 = xa; ra.ld1 = Ca; ra.C1 = Ca; ra.x2 = xb; ra.ld2 = Cb; ra.Cin = rb.c1.cin;
+      ra.B = B; ra.H = H; ra.W = W; ra.w1 = rb.c1.w; ra.w2 = rb.c2.w;
+      ra.wr = rb.has_res ? rb.res.w : nullptr; ra.ss = ss + rb.ss_off; ra.ss_ld = ss_total; ra.ldy = rb.dout;
+      const bool shapes = !q8pair && rb.dout == 64 && rb.c2.cin == 64 && rb.c1.kh == 3 && rb.c2.kh == 3 &&
+                          !rb.c1.dual && !rb.c2.dual && !rb.c1.kwp && !rb.c2.kwp && rb.c1.cin_real == Ca + Cb &&
+                          (!rb.has_res || (!rb.res.dual && !rb.res.b && rb.res.cin == rb.c1.cin)) &&
+                          !rb.c1.b && !rb.c2.b && rb.ss_off % 4 == 0 && ss_total % 4 == 0 && !no_res_fuse();
+      if (shapes && rbfuse_ok(ra) && rbfuse_pays(ra)) {
+        T* o = r.alloc<T>(M * rb.dout);
+        ra.y = o;
+        const double fl = 2.0 * M * 64 * 9 * (rb.c1.cin_real + 64) + (rb.has_res ? 2.0 * M * 64 * rb.c1.cin_real : 0.0);
+        r.flops += fl;
+        Profiler* p = r.prof;
+        const bool timed = p && (p->kernel_id == Profiler::ALL || p->kernel_id == 350);
+        if (r.dry) {
+          if (timed) p->used++;
+          return o;
+        }
+        if (!rb.c1.w || !rb.c2.w || (rb.has_res && !rb.res.w)) throw Error(DAC_E_STATE, "conv weight not loaded");
+        if (timed) {
+          if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
+          HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
+        }
+        rbfuse<T>(ra, r.st);
+        if (timed) {
+          HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
+          p->used++;
+          p->launches++;
+          p->flops += fl;
+          if (p->kernel_id == Profiler::ALL) {
+            char lab[160];
+            snprintf(lab, sizeof lab, "c350 %3dx%-3d  ResBlock %4d->%-4d fused", H, W, rb.c1.cin_real, rb.dout);
+            p->labels.push_back(lab);
+            p->lflops.push_back(fl);
+          }
+          // Algorithmic HBM bytes: x in, y out.
+          p->bytes += 2.0 * M * (rb.c1.cin_real + rb.dout);
+        }
+        return o;
+      }
+    }
     T* h1 = r.alloc<T>(M * rb.dout);
     Epi e1;
     e1.ss = ss + rb.ss_off; e1.ss_ld = ss_total; e1.act = ACT_SILU;

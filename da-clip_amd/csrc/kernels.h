@@ -129,6 +129,24 @@ inline bool conv3w_ok(const ConvArgs& a) {
 }
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int stride, int pad, hipStream_t st);
+// Fused ResBlock (rbfuse.hip, 16-bit types; module_util.py:132-153): block1 (3x3 Cin -> 64,
+// per-image scale / shift, SiLU) and block2 (3x3 64 -> 64, SiLU) + residual in one launch, h (and
+// the 1x1 res_conv output) never leaving LDS. Cin = 64 (residual = x) or 128 (x1 | x2 = torch.cat
+// of two 64-channel tensors, or one 128-channel tensor; residual = x w_res^T).
+struct RbArgs {
+  const void* x1; const void* x2;
+  int ld1, ld2, C1, Cin;
+  int B, H, W;
+  const void* w1;          // [64][3][3][Cin]
+  const void* w2;          // [64][3][3][64]
+  const void* wr;          // [64][Cin] (Cin = 128) or null
+  const float* ss; int ss_ld;    // scale [b * ss_ld + n], shift [b * ss_ld + 64 + n]
+  void* y; int ldy;
+};
+bool rbfuse_pays(const RbArgs& a);
+bool rbfuse_ok(const RbArgs& a);
+template <typename T>
+void rbfuse(const RbArgs& a, hipStream_t st);
 // Register-stationary 3x3 conv, 64 -> 64 (conv3r.hip, 16-bit types): the shapes it serves
 // (DAC_CONV3R=0 turns it off) and its launcher.
 bool conv3r_ok(const ConvArgs& a);

@@ -1,0 +1,431 @@
+// rbfuse.hip — the UNet's ResBlock as ONE kernel at the 256x256 level (16-bit types):
+//   h = SiLU((x * W1) (1 + scale) + shift),  y = SiLU(h * W2) + res,
+//   res = x (Cin = 64) or x * Wres (Cin = 128, the 1x1 res_conv)      (module_util.py:115-153)
+// with h and the res_conv output kept in LDS: per ResBlock the level moves x in and y out
+// through HBM (2 x 67 MB at B = 8) instead of x, h, y2 (and x again as the residual) between two
+// conv launches (≈ 370-470 MB), which made the conv3r pair HBM-bound.
+//
+// Structure (conv3r.hip's register-stationary convs, two of them in one block):
+//   * a block (8 waves, one block per CU) owns a strip of SW output columns (128 for Cin 64,
+//     64 for Cin 128) of one image over RB output rows;
+//   * waves 0-3 run block1, waves 4-7 block2; wave w and w + 4 share a SIMD, so one conv's
+//     epilogue overlaps the other's MFMAs. Each wave keeps its weight slice in VGPRs: block1
+//     32 channels x 576 (Cin 64) or 16 channels x 1152 + the 16 x 128 res_conv slice (Cin 128),
+//     block2 32 (Cin 64 strips) or 16 (Cin 128 strips) channels x 576;
+//   * step t: block1 computes h row t (x rows t-1 .. t+1 from a 5-slot LDS ring fed by LDS-DMA one
+//     step ahead) into a 4-slot LDS ring of h rows (and, Cin 128, the res_conv row into a 3-slot
+//     ring); block2 computes output row t - 2 from h rows t-3 .. t-1 and adds the residual (x row
+//     t - 2, still in the x ring, or the res_conv row); one barrier per step;
+//   * block2's 3x3 needs h one column beyond each side of the strip: block1's waves compute
+//     those two columns as one extra 16-lane tile (split over the two pixel groups' waves by
+//     channel tile) (lanes 0-7: column x0 - 1, lanes
+//     8-15: column x0 + SW, duplicated) from x columns x0 - 2 .. x0 + SW + 1 — the same K order as
+//     the neighbouring strip's interior pixels, so the values are bit-identical to theirs. Columns
+//     and rows outside the image are zero (block2's padding), written as zeros.
+// Every output is the same ordered MFMA sum (kernel row, 32-channel chunk, tap) and the same
+// epilogue arithmetic as conv3r's two launches, so the fused block is bit-identical to the pair
+// (tests/test_conv_kernels.py: convbench rbf), whatever the band height or batch.
+#include "conv_impl.h"
+
+namespace dac {
+
+namespace {
+constexpr unsigned RBF_OOB = 0x80000000u;
+DEV int rbf_phys(int p) { return p ^ ((p >> 2) & 1); }
+DEV int rbf_chunk(int P, int q) { return q ^ ((P >> 2) & 7); }
+// Byte offset of (halo pixel p, 16-byte channel chunk q) in a 64-channel row image.
+DEV int rbf_off(int p, int q) {
+  const int P = rbf_phys(p);
+  return P * 128 + (rbf_chunk(P, q) << 4);
+}
+
+template <int CIN> struct RBF {
+  static constexpr int NSRC = CIN / 64;
+  static constexpr int SW = CIN == 64 ? 128 : 64;     // strip width
+  static constexpr int NG = SW / 64;                  // 64-pixel groups
+  static constexpr int JT = NG;                       // 16-row MFMA tiles per wave (both convs)
+  static constexpr int OPW = 16 * JT;                 // output channels per wave
+  static constexpr int NGW = 4 / NG;                  // waves per pixel group
+  static constexpr int NC1 = CIN / 32;                // block1 K chunks per tap
+  static constexpr int XPX = SW + 4, NIX = (XPX + 7) / 8, XHALF = NIX * 1024, XROW = NSRC * XHALF;
+  static constexpr int HPX = SW + 2, NIH = (HPX + 7) / 8, HROW = NIH * 1024;
+  static constexpr int XS = 5, HS = 4;
+  static constexpr int OFF_H = XS * XROW, OFF_T = OFF_H + HS * HROW;
+  static constexpr int SMEM = OFF_T + 512;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+template <typename T> DEV void store4_g(T* p, const float* v) {
+  typedef T T4 __attribute__((ext_vector_type(4)));
+  T4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
+  *reinterpret_cast<T4*>(p) = o;
+}
+template <typename T> DEV void st_lds(char* p, const float* v, int n) {
+  if (n == 8) {
+    typedef T T8 __attribute__((ext_vector_type(8)));
+    T8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (T)v[e];
+    *reinterpret_cast<T8*>(p) = o;
+  } else {
+    typedef T T4 __attribute__((ext_vector_type(4)));
+    T4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
+    *reinterpret_cast<T4*>(p) = o;
+  }
+}
+}  // namespace
+
+// DAC_RBFUSE: 0 off, 1 (default) where it pays (rbfuse_pays), 2 wherever it applies (A/B runs).
+static int g_rbfuse_on = getenv("DAC_RBFUSE") ? atoi(getenv("DAC_RBFUSE")) : 1;
+extern "C" void dac_rbfuse_enable(int on) { g_rbfuse_on = on; }
+
+// The fused block saves HBM traffic but costs MFMA work: block1 recomputes (RB + 2) / RB h rows
+// per band and a 16-lane edge tile for the two halo columns (+12.5 % per wave at SW 128, +25 % at
+// SW 64). Measured against the conv3r pair (convbench rbf, fp16 on MI355X, us):
+//   64 -> 64     B 1: 29.2 vs 33.1   B 2: 38.3 vs 42.3   B 4: 56.2 vs 59.0   B 8: 95.8 vs 91.0
+//   64|64 -> 64  B 1: 35.0 vs 40.2   B 2: 52.4 vs 55.5   B 4: 87.7 vs 81.9   B 8: 176.5 vs 138.6
+// (256 x 256 images): it wins while the pair's launches under-fill the chip and loses once the
+// pair is MFMA-bound rather than HBM-bound — at B 8 the pair moves 3.5 TB/s, not the ~6 it would
+// need to be limited by HBM. Both forms are bit-identical, so this batch-dependent choice leaves
+// every image's output unchanged (tests/test_hip_parity.py batch tests).
+bool rbfuse_pays(const RbArgs& a) {
+  const size_t px = (size_t)a.B * a.H * a.W, img = (size_t)256 * 256;
+  return g_rbfuse_on == 2 || px <= (a.Cin == 64 ? 4 : 2) * img;
+}
+
+bool rbfuse_ok(const RbArgs& a) {
+  if (!g_rbfuse_on || !(a.Cin == 64 || a.Cin == 128)) return false;
+  const int SW = a.Cin == 64 ? RBF<64>::SW : RBF<128>::SW;
+  if ((a.Cin == 128) != (a.wr != nullptr)) return false;
+  const bool one = a.x2 == nullptr || a.C1 >= a.Cin;
+  if (!one && !(a.C1 == 64 && a.Cin == 128 && a.ld2 % 8 == 0)) return false;
+  // (The caller guarantees 16-byte aligned scale / shift rows; no pointer is tested here, so
+  // the engine's dry planning run takes the same decision as the live one.)
+  return a.W % SW == 0 && a.W >= 256 && a.ld1 % 8 == 0 && a.ldy % 8 == 0 && a.ss_ld % 4 == 0 &&
+         ((size_t)a.H * a.W + 1) * a.ld1 * 2 < ((size_t)1 << 31) &&
+         (one || ((size_t)a.H * a.W + 1) * a.ld2 * 2 < ((size_t)1 << 31));
+}
+
+template <typename T, int CIN>
+__global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
+  using G = RBF<CIN>;
+  constexpr int JT = G::JT, SW = G::SW, NC1 = G::NC1, EV = 4 * JT;
+  constexpr bool FUSE = CIN == 128;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool conv1 = wave < 4;
+  const int wl = wave & 3;
+  const int g = wl / G::NGW, ob = G::OPW * (wl % G::NGW);
+  const int lr = lane & 15, lg = lane >> 4;
+  const int nb = ob + EV * lg;                    // the lane's first output channel
+
+  const int nbands = gridDim.x;
+  const int bid = nbands % 8 == 0 ? (blockIdx.x & 7) * (nbands >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const int S = a.W / SW, nrb = a.H / RB;
+  const int strip = bid % S, rb = (bid / S) % nrb, img = bid / (S * nrb);
+  const int x0 = strip * SW, r0 = rb * RB;
+  const bool lpad = x0 == 0, rpad = x0 + SW == a.W;
+
+  char* xring = smem;
+  char* hring = smem + G::OFF_H;
+  float* terms = reinterpret_cast<float*>(smem + G::OFF_T);
+  // Block1's folded (1 + scale, shift) of this image, in the log2 domain of silu_log2.
+  if (threadIdx.x < 64) {
+    const int n = threadIdx.x;
+    float sc = 1.f + a.ss[(size_t)img * a.ss_ld + n], sh = a.ss[(size_t)img * a.ss_ld + 64 + n];
+    epi_fold(0.f, sc, sh, true);
+    terms[n] = sc;
+    terms[64 + n] = sh;
+  }
+
+  // x ring: halo pixel p = input column x0 - 2 + p; LDS-DMA by block1's waves (as conv3r).
+  const bool one = a.x2 == nullptr || a.C1 >= a.Cin;
+  const int ldb0 = a.ld1 * 2, ldb1 = one ? ldb0 : a.ld2 * 2;
+  const char* xsrc0 = reinterpret_cast<const char*>(a.x1) + (size_t)img * a.H * a.W * ldb0 - 2 * ldb0;
+  const char* xsrc1 = one ? xsrc0 + 128
+                          : reinterpret_cast<const char*>(a.x2) + (size_t)img * a.H * a.W * ldb1 - 2 * ldb1;
+  const int xb0 = (a.H * a.W + 2) * ldb0, xb1 = (a.H * a.W + 2) * ldb1 - (one ? 128 : 0);
+  auto xslot = [&](int row) { return xring + ((row + 10) % G::XS) * G::XROW; };
+  auto issue_x = [&](int ir) {
+    const bool ok = (unsigned)ir < (unsigned)a.H;
+    char* dst = xslot(ir);
+    // (The lane index through an empty asm: the per-lane DMA offsets are recomputed per row
+    // instead of being hoisted into registers for the kernel's lifetime — VGPRs are the limit.)
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    constexpr int NQ = G::NSRC * G::NIX;
+#pragma unroll
+    for (int k = 0; k < (NQ + 3) / 4; ++k) {
+      const int q = wl + 4 * k;
+      if (q < NQ) {
+        const bool h1 = q >= G::NIX;
+        const int qq = h1 ? q - G::NIX : q, ldb = h1 ? ldb1 : ldb0;
+        const int P = 8 * qq + (lane >> 3), p = rbf_phys(P);
+        const bool pad = p >= SW + 4 || (lpad && p < 2) || (rpad && p >= SW + 2);
+        const int v = (ok && !pad) ? p * ldb + rbf_chunk(P, lane & 7) * 16 : (int)RBF_OOB;
+        buf_lds16(h1 ? xsrc1 : xsrc0, h1 ? xb1 : xb0, dst + q * 1024, v, ok ? (ir * a.W + x0) * ldb : 0);
+      }
+    }
+  };
+
+  // Quad bases of the interior B fragments (conv3r's closed form) in a ring image whose halo
+  // pixel of output column x0 + 64 g + 4 lr + s is hp0 + 64 g + 4 lr + s.
+  auto quad_base = [&](int u) {
+    const int q = lr + u;
+    return (64 * g + 4 * q) * 128 + ((q & 1) << 7) + ((lg ^ ((16 * g + q) & 7)) << 4);
+  };
+  const int bq0 = quad_base(0), bq1 = quad_base(1);
+  // Fragment offset of halo pixel 64 g + 4 lr + s (s = 0 .. 7) and chunk parity c, from the two
+  // quad bases as (re)defined per fragment group: the bases pass through an empty asm at each
+  // group, so the compiler derives the six offsets there instead of hoisting all twelve (and the
+  // edge tile's) into registers for the kernel's lifetime (they spilled: VGPRs are the limit).
+  auto fresh = [](int v) { asm volatile("" : "+v"(v)); return v; };
+  auto foff = [&](int b0, int b1, int s, int c) {
+    const int base = s < 4 ? b0 : b1;              // (s < 8)
+    return base ^ ((s & 3) << 7) ^ (c << 6);
+  };
+
+  const int nsteps = RB + 3;                      // t = r0 - 1 .. r0 + RB + 1
+  if (conv1) {
+    // ------------------------------------------------------------------ block1 (+ res_conv)
+    u32x4 W[9 * NC1][JT];
+    {
+      const T* w = reinterpret_cast<const T*>(a.w1);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) {
+        const int n = JT == 2 ? ob + 8 * (lr >> 2) + 4 * j + (lr & 3) : ob + lr;
+#pragma unroll
+        for (int ks = 0; ks < 9 * NC1; ++ks)
+          W[ks][j] = *reinterpret_cast<const u32x4*>(w + (size_t)n * (9 * CIN) + (ks / NC1) * CIN + (ks % NC1) * 32 + 8 * lg);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0) here, not inside the step loop
+    // Edge tile: lanes 0-7 h column x0 - 1 (x halo pixels 0..2), lanes 8-15 h column x0 + SW (x
+    // halo pixels SW + 1 .. SW + 3), read in the group loop below. With two pixel groups (JT 2)
+    // group g computes its channel tiles' j = g half of it, so the extra MFMAs are spread over all
+    // four SIMDs instead of two; with one group (JT 1) every wave computes its own.
+    issue_x(r0 - 2);
+    issue_x(r0 - 1);
+    issue_x(r0);
+    for (int st = 0; st < nsteps; ++st) {
+      const int t = r0 - 1 + st;
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // x row t + 1 landed; h writes done
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 2 <= r0 + RB + 1) issue_x(t + 2);
+      if (t > r0 + RB) continue;                   // (block2's last step)
+      char* hdst = hring + (t & 3) * G::HROW;
+      if ((unsigned)t >= (unsigned)a.H) {
+        // h rows outside the image: block2's zero padding.
+        for (int i = threadIdx.x; i < G::HROW / 16; i += 256) reinterpret_cast<u32x4*>(hdst)[i] = u32x4{0u, 0u, 0u, 0u};
+        continue;
+      }
+      f32x4 acc[4][JT], acce = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const char* xr = xslot(t + kh - 1);
+#pragma unroll
+        for (int c32 = 0; c32 < NC1; ++c32) {
+          __builtin_amdgcn_sched_barrier(0);
+          const char* hr = xr + (c32 >> 1) * G::XHALF;
+          const int c = c32 & 1;
+          const int b0 = fresh(bq0), b1 = fresh(bq1);
+          u32x4 F[6];
+#pragma unroll
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, s + 1, c));
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < JT; ++j) Mma<T>::run(acc[i][j], W[(kh * 3 + kw) * NC1 + c32][j], F[i + kw]);
+          {
+            const int le = fresh(lr);
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (rbf_off(le < 8 ? SW + 1 + kw : kw, lg) ^ (c << 6)));
+              if (JT == 1 || g == 0) Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][0], E);
+              else Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][JT - 1], E);
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // Epilogue -> LDS: h (scale / shift, SiLU) at halo pixel 64 g + 4 lr + i + 1; the lane's
+      // EV channels nb .. are 16-byte chunk nb / 8 (EV = 8) or its half (EV = 4).
+      float fs[EV], fh[EV];
+      {
+        const f32x4* tv = reinterpret_cast<const f32x4*>(terms + nb);
+#pragma unroll
+        for (int q = 0; q < JT; ++q) {
+          const f32x4 s0 = tv[q], h0 = tv[16 + q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { fs[4 * q + e] = s0[e]; fh[4 * q + e] = h0[e]; }
+        }
+      }
+      const int q16 = nb >> 3, half8 = (nb >> 2) & 1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v[EV];
+#pragma unroll
+        for (int e = 0; e < EV; ++e) v[e] = silu_log2(fmaf(acc[i][e >> 2][e & 3], fs[e], fh[e]));
+        st_lds<T>(hdst + rbf_off(64 * g + 4 * lr + i + 1, q16) + half8 * 8, v, EV);
+      }
+      {
+        const bool zero = lr < 8 ? rpad : lpad;    // outside the image: padding
+        const int jg = JT == 1 ? 0 : g;            // the edge tile's channel half (EV 8) or all (EV 4)
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sc = jg ? fs[EV - 4 + e] : fs[e], sh = jg ? fh[EV - 4 + e] : fh[e];
+          v[e] = zero ? 0.f : silu_log2(fmaf(acce[e], sc, sh));
+          // (An empty asm between SiLU's last multiply and the f16 conversion: here the compiler
+          // otherwise contracts the two into v_fma_mixlo_f16 — one rounding instead of the
+          // interior's two — and the edge columns differed from conv3r's h in rare last bits.)
+          asm volatile("" : "+v"(v[e]));
+        }
+        st_lds<T>(hdst + rbf_off(lr < 8 ? SW + 1 : 0, q16) + (half8 + jg) * 8, v, 4);
+      }
+    }
+  } else {
+    // ------------------------------------------------------------------ block2 (+ residual)
+    u32x4 W[18][JT];
+    u32x4 WR[FUSE ? NC1 : 1][JT];
+    {
+      const T* w = reinterpret_cast<const T*>(a.w2);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) {
+        const int n = JT == 2 ? ob + 8 * (lr >> 2) + 4 * j + (lr & 3) : ob + lr;
+#pragma unroll
+        for (int ks = 0; ks < 18; ++ks)
+          W[ks][j] = *reinterpret_cast<const u32x4*>(w + (size_t)n * 576 + (ks >> 1) * 64 + (ks & 1) * 32 + 8 * lg);
+        if constexpr (FUSE) {
+          const T* wr = reinterpret_cast<const T*>(a.wr);
+#pragma unroll
+          for (int c = 0; c < NC1; ++c) WR[c][j] = *reinterpret_cast<const u32x4*>(wr + (size_t)n * CIN + c * 32 + 8 * lg);
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    T* y = reinterpret_cast<T*>(a.y);
+    const int q16 = nb >> 3, half8 = (nb >> 2) & 1;
+    for (int st = 0; st < nsteps; ++st) {
+      const int t = r0 - 1 + st, u = t - 2;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (u < r0) continue;
+      f32x4 acc[4][JT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const char* hr = hring + ((u + kh - 1) & 3) * G::HROW;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int b0 = fresh(bq0), b1 = fresh(bq1);
+          u32x4 F[6];
+#pragma unroll
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, s, c));
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < JT; ++j) Mma<T>::run(acc[i][j], W[(kh * 3 + kw) * 2 + c][j], F[i + kw]);
+        }
+      }
+      // Cin 128: the 1x1 res_conv of x row u (still in the x ring; centre pixels, the same K order
+      // as conv3r's fused form) — computed here by block2's waves, whose block1-free VGPRs hold
+      // its weights, and never stored.
+      f32x4 accr[FUSE ? 4 : 1][JT];
+      if constexpr (FUSE) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < JT; ++j) accr[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const char* xr = xslot(u);
+#pragma unroll
+        for (int c32 = 0; c32 < NC1; ++c32) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int b0 = fresh(bq0), b1 = fresh(bq1);
+          const char* hr = xr + (c32 >> 1) * G::XHALF;
+          u32x4 F[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) F[i] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, i + 2, c32 & 1));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < JT; ++j) Mma<T>::run(accr[i][j], WR[c32][j], F[i]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // Epilogue: SiLU + residual (x row u from the x ring, or the res_conv output).
+      const size_t m0 = ((size_t)img * a.H + u) * a.W + x0 + 64 * g + 4 * lr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v[EV];
+#pragma unroll
+        for (int e = 0; e < EV; ++e) v[e] = silu_log2(acc[i][e >> 2][e & 3] * kL2E);
+        if constexpr (FUSE) {
+          // The res_conv output is a T tensor in the unfused form: round it to T, then add it
+          // exactly as conv3r's residual epilogue does (add_pair: no contraction into SiLU's
+          // last multiply, which f16's fma_mix form rules out and a plain += would allow).
+#pragma unroll
+          for (int w2 = 0; w2 < EV / 2; ++w2) {
+            const T lo = from_f<T>(accr[i][(2 * w2) >> 2][(2 * w2) & 3]);
+            const T hi = from_f<T>(accr[i][(2 * w2 + 1) >> 2][(2 * w2 + 1) & 3]);
+            const unsigned u = (unsigned)__builtin_bit_cast(unsigned short, lo) |
+                               ((unsigned)__builtin_bit_cast(unsigned short, hi) << 16);
+            add_pair<T>(u, v[2 * w2], v[2 * w2 + 1]);
+          }
+          store4_g<T>(y + (m0 + i) * a.ldy + nb, v);
+        } else {
+          const u32x4 r = *reinterpret_cast<const u32x4*>(xslot(u) + rbf_off(64 * g + 4 * lr + i + 2, q16));
+#pragma unroll
+          for (int w2 = 0; w2 < 4; ++w2) add_pair<T>(r[w2], v[2 * w2], v[2 * w2 + 1]);
+          store_vec<T>(y + (m0 + i) * a.ldy + nb, v);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Band height: the largest divisor of H giving >= 256 bands (one block per CU), else 1.
+static int rbfuse_rb(const RbArgs& a, int SW) {
+  const long rows = (long)a.B * a.H * (a.W / SW);
+  int rb = (int)(rows / 256);
+  if (rb < 1) rb = 1;
+  if (rb > a.H) rb = a.H;
+  while (a.H % rb) --rb;
+  return rb;
+}
+
+template <typename T>
+void rbfuse(const RbArgs& a, hipStream_t st) {
+  if (!rbfuse_ok(a)) abort();
+  if (a.Cin == 64) {
+    const int rb = rbfuse_rb(a, RBF<64>::SW);
+    rbfuse_kernel<T, 64><<<a.B * (a.H / rb) * (a.W / RBF<64>::SW), 512, 0, st>>>(a, rb);
+  } else {
+    const int rb = rbfuse_rb(a, RBF<128>::SW);
+    rbfuse_kernel<T, 128><<<a.B * (a.H / rb) * (a.W / RBF<128>::SW), 512, 0, st>>>(a, rb);
+  }
+}
+template void rbfuse<bf16>(const RbArgs&, hipStream_t);
+template void rbfuse<f16>(const RbArgs&, hipStream_t);
+
+}  // namespace dac

@@ -98,3 +98,18 @@ def test_row_phase_upsample_conv_matches_plain():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
     assert len(rows) == 3 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+
+
+@pytest.mark.gpu
+def test_fused_resblock_matches_conv3r_pair():
+    """The 256x256 ResBlock as one launch (rbfuse.hip: block1 3x3 + scale/shift + SiLU, block2
+    3x3 + SiLU + residual, Cin 128's 1x1 res_conv too; module_util.py:115-153) against the two
+    conv3r launches it replaces, on random bf16 data: bit-identical (same ordered MFMA sums and
+    epilogue arithmetic) for one and two sources, ld2 != C2, B 1..8 and Cin 64 / 128. Timing
+    lines (pair vs fused) are printed; the engine takes the fused form only where it pays."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "rbf", "3"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    rows = [l for l in out.stdout.splitlines() if "check" in l]
+    assert len(rows) == 18 and all(l.rstrip().endswith("check OK") for l in rows), out.stdout

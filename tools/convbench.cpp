@@ -17,6 +17,7 @@ using namespace dac;
 extern "C" void dac_conv3_force(int v);
 extern "C" void dac_conv2_force(int v);
 extern "C" void dac_conv3r_enable(int on);
+extern "C" void dac_rbfuse_enable(int on);
 typedef __bf16 bf16;
 
 struct Shape { const char* name; int B, H, W, cin, cout, kh, s, p, up, act, ss, res, kwp = 0, bias = 0; };
@@ -903,7 +904,109 @@ static int c3r_check(int iters) {
   return bad ? 1 : 0;
 }
 
+// ---- fused ResBlock (rbfuse.hip) check: the single launch must reproduce the two-launch pair
+// (block1 3x3 + scale/shift + SiLU [+ fused 1x1 res_conv], block2 3x3 + SiLU + residual) bit for
+// bit — both are the same ordered MFMA sums and epilogue arithmetic — and is timed against it.
+template <typename E> __global__ void fill_rand_t(E* p, size_t n, uint32_t seed, float scale) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed * 0x9e3779b9u;
+  h ^= h >> 15; h *= 0x2c1b3c6du; h ^= h >> 12; h *= 0x297a2d39u; h ^= h >> 15;
+  p[i] = (E)(((h & 0xffff) / 65535.f - 0.5f) * scale);
+}
+
+template <typename E> static int rbf_check(int iters, const char* tn) {
+  struct Q { const char* name; int B, H, W, c1, c2, ld2; };
+  const Q shapes[] = {
+    {"rbf 64->64 x1 256^2", 1, 256, 256, 64, 0, 0},
+    {"rbf 64|64->64 x1 256^2", 1, 256, 256, 64, 64, 64},
+    {"rbf 64->64 x2 256^2", 2, 256, 256, 64, 0, 0},
+    {"rbf 128->64 256x512", 1, 256, 512, 128, 0, 0},
+    {"rbf 64|64->64 256^2 ld2 96", 2, 256, 256, 64, 64, 96},
+    {"rbf 64->64 B4 256^2", 4, 256, 256, 64, 0, 0},
+    {"rbf 64|64->64 B4 256^2", 4, 256, 256, 64, 64, 64},
+    {"rbf 64->64 B8 256^2", 8, 256, 256, 64, 0, 0},
+    {"rbf 64|64->64 B8 256^2", 8, 256, 256, 64, 64, 64},
+  };
+  int bad = 0;
+  for (const Q& q : shapes) {
+    const int cin = q.c1 + q.c2, ld1 = q.c1, ld2 = q.c2 ? q.ld2 : 0;
+    const bool res = cin == 128;
+    const size_t npx = (size_t)q.B * q.H * q.W;
+    E *x1, *x2 = nullptr, *w1, *w2, *wr, *h, *y2, *yu, *yf;
+    float* ss;
+    CK(hipMalloc(&x1, npx * ld1 * 2)); if (q.c2) CK(hipMalloc(&x2, npx * ld2 * 2));
+    CK(hipMalloc(&w1, (size_t)64 * 9 * cin * 2)); CK(hipMalloc(&w2, (size_t)64 * 576 * 2)); CK(hipMalloc(&wr, (size_t)64 * cin * 2));
+    CK(hipMalloc(&h, npx * 128)); CK(hipMalloc(&y2, npx * 128)); CK(hipMalloc(&yu, npx * 128)); CK(hipMalloc(&yf, npx * 128));
+    CK(hipMalloc(&ss, q.B * 128 * 4));
+    fill_rand_t<E><<<(npx * ld1 + 255) / 256, 256>>>(x1, npx * ld1, 21, 2.f);
+    if (q.c2) fill_rand_t<E><<<(npx * ld2 + 255) / 256, 256>>>(x2, npx * ld2, 22, 2.f);
+    fill_rand_t<E><<<(64 * 9 * cin + 255) / 256, 256>>>(w1, (size_t)64 * 9 * cin, 23, 0.1f);
+    fill_rand_t<E><<<(64 * 576 + 255) / 256, 256>>>(w2, (size_t)64 * 576, 24, 0.1f);
+    fill_rand_t<E><<<(64 * cin + 255) / 256, 256>>>(wr, (size_t)64 * cin, 25, 0.2f);
+    fill_rand_f<<<(q.B * 128 + 255) / 256, 256>>>(ss, q.B * 128, 26, 1.f);
+    void* zero; CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+    ConvArgs a1{};
+    a1.x1 = x1; a1.ld1 = ld1; a1.C1 = q.c1; a1.x2 = x2; a1.ld2 = ld2; a1.Cin = cin; a1.Hs = q.H; a1.Ws = q.W;
+    a1.B = q.B; a1.Ho = q.H; a1.Wo = q.W; a1.Cout = 64; a1.K = 9 * cin; a1.w = w1; a1.y = h; a1.ldy = 64;
+    a1.act = 1; a1.zero = zero; a1.ss = ss; a1.ss_ld = 128;
+    if (res) { a1.w2 = wr; a1.y2 = y2; a1.ldy2 = 64; }
+    ConvArgs a2{};
+    a2.x1 = h; a2.ld1 = 64; a2.C1 = 64; a2.Cin = 64; a2.Hs = q.H; a2.Ws = q.W; a2.B = q.B; a2.Ho = q.H; a2.Wo = q.W;
+    a2.Cout = 64; a2.K = 576; a2.w = w2; a2.y = yu; a2.ldy = 64; a2.act = 1; a2.zero = zero;
+    a2.res1 = res ? (const void*)y2 : (const void*)x1; a2.ldr1 = res ? 64 : ld1;
+    RbArgs rf{};
+    rf.x1 = x1; rf.ld1 = ld1; rf.C1 = q.c1; rf.x2 = x2; rf.ld2 = ld2; rf.Cin = cin; rf.B = q.B; rf.H = q.H; rf.W = q.W;
+    rf.w1 = w1; rf.w2 = w2; rf.wr = res ? wr : nullptr; rf.ss = ss; rf.ss_ld = 128; rf.y = yf; rf.ldy = 64;
+    dac_conv3_force(-1);
+    if (res && !conv_res_fusable(a1)) { printf("%-30s no fused res_conv kernel\n", q.name); bad++; continue; }
+    if (!rbfuse_ok(rf)) { printf("%-30s rbfuse_ok false\n", q.name); bad++; continue; }
+    auto pair = [&]() { conv<E>(a1, 3, 3, 1, 1, 0); conv<E>(a2, 3, 3, 1, 1, 0); };
+    auto fused = [&]() { rbfuse<E>(rf, 0); };
+    pair(); fused();
+    CK(hipDeviceSynchronize());
+    std::vector<uint16_t> hu(npx * 64), hf(npx * 64);
+    CK(hipMemcpy(hu.data(), yu, npx * 128, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hf.data(), yf, npx * 128, hipMemcpyDeviceToHost));
+    size_t diff = 0, first = (size_t)-1;
+    for (size_t i = 0; i < hu.size(); ++i) if (hu[i] != hf[i]) { if (!diff) first = i; ++diff; }
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    float ms[2];
+    for (int arm = 0; arm < 2; ++arm) {
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) { if (arm) fused(); else pair(); }
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms[arm], e0, e1));
+    }
+    const double fl = 2.0 * npx * 64 * 9 * (cin + 64) + (res ? 2.0 * npx * 64 * cin : 0.0);
+    printf("%s %-30s pair %7.1f us, fused %7.1f us (%6.1f TF/s)  %zu of %zu outputs differ", tn, q.name, ms[0] * 1e3 / iters,
+           ms[1] * 1e3 / iters, fl / (ms[1] * 1e-3 / iters) / 1e12, diff, hu.size());
+    if (diff) {
+      int shown = 0;
+      for (size_t i = 0; i < hu.size() && shown < 4; ++i)
+        if (hu[i] != hf[i]) {
+          const size_t m = i / 64;
+          printf("\n    px %zu (row %zu col %zu) ch %zu: pair %04x fused %04x", m, (m / q.W) % q.H, m % q.W, i % 64, hu[i], hf[i]);
+          ++shown;
+        }
+      printf("\n   ");
+      const size_t m = first / 64;
+      printf(" (first: pixel %zu (b %zu, row %zu, col %zu) ch %zu)", m, m / ((size_t)q.H * q.W), (m / q.W) % q.H, m % q.W, first % 64);
+    }
+    printf("  check %s\n", diff ? "FAIL" : "OK");
+    bad += diff != 0;
+    hipFree(x1); if (x2) hipFree(x2); hipFree(w1); hipFree(w2); hipFree(wr); hipFree(h); hipFree(y2); hipFree(yu);
+    hipFree(yf); hipFree(ss); hipFree(zero);
+  }
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "rbf")) {
+    const int it = argc > 2 ? atoi(argv[2]) : 20;
+    const int b = rbf_check<bf16>(it, "bf16");
+    return rbf_check<_Float16>(it, "f16 ") | b;
+  }
   if (argc > 1 && !strcmp(argv[1], "c3r")) return c3r_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
   if (argc > 1 && !strcmp(argv[1], "uph")) return uph_check(argc > 2 ? atoi(argv[2]) : 20);
