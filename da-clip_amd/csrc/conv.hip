@@ -9,7 +9,8 @@ namespace dac {
 int g_conv3_force = -1;
 int g_conv2_force = 0;
 // Tuning aid: DAC_CONV2_FORCE32=k forces 1x1 configuration k on the small-image GEMMs only
-// (Ho*Wo <= 1024: the SpatialTransformer level), for in-network sweeps.
+// (Ho*Wo <= 1024: the SpatialTransformer level; GEGLU projections keep their tile), for in-network
+// sweeps.
 int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 int g_conv3h_on = getenv("DAC_CONV3H") ? atoi(getenv("DAC_CONV3H")) : 0;

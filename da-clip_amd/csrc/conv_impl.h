@@ -632,7 +632,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
       // Own DMA of tile kt done (STAGES-2 younger tiles may stay in flight), then barrier.
       if constexpr (STAGES == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else if constexpr (STAGES == 3) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(AG + BG) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(2 * (AG + BG)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"((STAGES - 2) * (AG + BG)) : "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       issue(kt + STAGES - 1);                    // refills the slot read at iteration kt-1
@@ -2257,7 +2257,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
       }
       __builtin_trap();                          // conv_lnf_ok said a folding kernel takes it
     }
-    const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho * a.Wo <= 1024) ? g_conv2_force32 : g_conv2_force;
+    const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho * a.Wo <= 1024 && a.Ho * a.Wo >= 256 && a.ksplit <= 1 && a.act != ACT_GEGLU) ? g_conv2_force32 : g_conv2_force;
     if constexpr (KH == 1) if (f2 > 0) {
       switch (f2) {
         case 1: DAC_V2(256, 128, 4, 2, 3, 512)
@@ -2284,6 +2284,18 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
               return;
             }
           DAC_V2(64, 128, 2, 2, 3, 256)
+        case 17:
+        case 18:
+        case 19:
+          if constexpr (sizeof(T) == 2)
+            if (minimal(128) && a.Cout % 128 == 0) {
+              // Deep rings (in-flight depth probe): 64x128 x 6 stages, 128x128 x 4 / 5 stages.
+              if (f2 == 17) conv2_kernel<T, 64, 128, 2, 2, 6, KH, KW, S, P, EPI_SWAP><<<dim3((Mg + 63) / 64, a.Cout / 128, gz), 256, 0, st>>>(a);
+              else if (f2 == 18) conv2_kernel<T, 128, 128, 2, 2, 4, KH, KW, S, P, EPI_SWAP><<<dim3((Mg + 127) / 128, a.Cout / 128, gz), 256, 0, st>>>(a);
+              else conv2_kernel<T, 128, 128, 2, 2, 5, KH, KW, S, P, EPI_SWAP><<<dim3((Mg + 127) / 128, a.Cout / 128, gz), 256, 0, st>>>(a);
+              return;
+            }
+          DAC_V2(64, 128, 2, 2, 2, 256)
         case 14:
         case 15:
         case 16:

@@ -633,6 +633,10 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
     conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
   } else {
     conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
+    // Diagnostic (DAC_DUP1X1=1): the 32x32-level 1x1 GEMMs run twice back to back (idempotent:
+    // the output never aliases an input), to separate a launch's cold-input cost in the trace.
+    static const bool dup = getenv("DAC_DUP1X1") && atoi(getenv("DAC_DUP1X1")) != 0;
+    if (dup && cw.kh == 1 && a.Ho * a.Wo <= 1024 && a.Ho * a.Wo >= 256 && a.ksplit <= 1) conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
   }
   emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
   if (fused) emu_round<T>(r, e.y2, e.ldy2, (size_t)M, cw.cout);
