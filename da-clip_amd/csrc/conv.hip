@@ -14,6 +14,8 @@ int g_conv2_force = 0;
 int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 int g_conv3h_on = getenv("DAC_CONV3H") ? atoi(getenv("DAC_CONV3H")) : 0;
+int g_c3i_st = getenv("DAC_C3I_ST") ? atoi(getenv("DAC_C3I_ST")) : 3;
+extern "C" void dac_c3i_st(int v) { g_c3i_st = v; }
 extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
 extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }
 

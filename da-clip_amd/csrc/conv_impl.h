@@ -1435,6 +1435,16 @@ extern int g_conv2_force;     // 1x1 v2 configuration override (convbench), 0 = 
 extern int g_conv2_force32;   // the same, small images only (DAC_CONV2_FORCE32)
 extern int g_conv3_buf;       // v4 buffer-resource DMA (FL bit 10); DAC_CONV3_BUF=0 disables
 extern int g_conv3h_on;       // v6 2-D halo kernel: 0 off, 1 measured-faster shapes, 2 all (DAC_CONV3H)
+// Ring depth of the plain v4 swapped tiles (no fused res_conv, no phase form) when the grid is at
+// most one block per CU (the 64x64 / 32x32 levels at B = 8): with no co-resident block to cover a
+// stage's DMA, deeper rings keep more of it in flight (DAC_C3I_ST = 2 / 3 / 4; 3 measured best: 32x32
+// 256->256 21.6 -> 18.9 us, 64x64 128->128 18.2 -> 17.6 us in the network, +0.45 % images/s). The stage count only
+// buffers: every output is the same ordered sum, so the choice leaves results bit-identical.
+extern int g_c3i_st;
+inline int c3i_small_st(const ConvArgs& a, int BM) {
+  const long tiles = (long)a.B * a.Ho * a.Wo / BM * ((a.Cout + 63) / 64);
+  return tiles <= 256 ? g_c3i_st : 2;
+}
 inline bool conv3h_pick(const ConvArgs& a) {
   return g_conv3h_on == 2 || (g_conv3h_on == 1 && a.Cin >= 128 && !a.res1 && !a.res2 && !a.bbias);
 }
@@ -2148,6 +2158,10 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
             if (a.Cout % 64 == 0 && nb && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
             abort();                                  // conv_res_fusable promised a fused kernel
+          } else if (a.Cout % 64 == 0 && nb && c3i_small_st(a, 256) == 3 && conv3i_try<T, 256, 64, 4, 1, 64, 3, 12 | 1024>(a, st)) {
+            return;
+          } else if (a.Cout % 64 == 0 && nb && c3i_small_st(a, 256) == 4 && conv3i_try<T, 256, 64, 4, 1, 64, 4, 12 | 1024>(a, st)) {
+            return;
           } else if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024>(a, st)) {
             return;
           } else if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12>(a, st)) {
@@ -2162,6 +2176,8 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         // convbench but 3 % slower in the network.)
         if constexpr (sizeof(T) == 2)
           if (a.Cout <= 256 && a.Cout % 64 == 0) {
+            if (g_conv3_buf && c3i_small_st(a, 128) == 3 && conv3i_try<T, 128, 64, 4, 1, 64, 3, 12 | 1024>(a, st)) return;
+            if (g_conv3_buf && c3i_small_st(a, 128) == 4 && conv3i_try<T, 128, 64, 4, 1, 64, 4, 12 | 1024>(a, st)) return;
             if (g_conv3_buf && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 1024>(a, st)) return;
             if (conv3i_try<T, 128, 64, 4, 1, 64, 2, 12>(a, st)) return;
           }

@@ -113,3 +113,15 @@ def test_fused_resblock_matches_conv3r_pair():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
     assert len(rows) == 18 and all(l.rstrip().endswith("check OK") for l in rows), out.stdout
+
+
+@pytest.mark.gpu
+def test_small_grid_ring_depth_bit_identical():
+    """The one-block-per-CU 3x3 v4 shapes (64x64 128->128, 32x32 256->256 at B = 8; module_util.py
+    :111-153) run a 3-stage LDS ring by default (DAC_C3I_ST): a 2-, 3- and 4-stage ring must give
+    bit-identical outputs (the stage count only buffers the same ordered MFMA sum)."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "st", "3"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert "c3i st: OK" in out.stdout and "MISMATCH" not in out.stdout, out.stdout

@@ -1001,7 +1001,61 @@ template <typename E> static int rbf_check(int iters, const char* tn) {
   return bad ? 1 : 0;
 }
 
+extern "C" void dac_c3i_st(int v);
+// Small-grid v4 ring depth (DAC_C3I_ST): time ST = 2 / 3 / 4 on the one-block-per-CU 3x3 shapes and
+// require bit-identical outputs (the stage count only buffers the same ordered sum).
+static int c3i_st_check(int iters) {
+  struct Q { const char* name; int B, H, W, cin, cout, ss, res; };
+  const Q shapes[] = {
+    {"64x64 128->128 ss+silu", 8, 64, 64, 128, 128, 1, 0},
+    {"64x64 128->128 silu+res", 8, 64, 64, 128, 128, 0, 1},
+    {"32x32 256->256 ss+silu", 8, 32, 32, 256, 256, 1, 0},
+    {"32x32 256->256 silu+res", 8, 32, 32, 256, 256, 0, 1},
+  };
+  int bad = 0;
+  for (const Q& q : shapes) {
+    const size_t npx = (size_t)q.B * q.H * q.W, nw = (size_t)q.cout * 9 * q.cin;
+    bf16 *x, *w, *y, *res; float *ss, *bias; void* zero;
+    CK(hipMalloc(&x, npx * q.cin * 2)); CK(hipMalloc(&w, nw * 2)); CK(hipMalloc(&y, npx * q.cout * 2));
+    CK(hipMalloc(&res, npx * q.cout * 2)); CK(hipMalloc(&ss, q.B * 2 * q.cout * 4)); CK(hipMalloc(&bias, q.cout * 4));
+    CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+    fill_rand<<<(npx * q.cin + 255) / 256, 256>>>(x, npx * q.cin, 21, 2.f);
+    fill_rand<<<(nw + 255) / 256, 256>>>(w, nw, 22, 0.1f);
+    fill_rand<<<(npx * q.cout + 255) / 256, 256>>>(res, npx * q.cout, 23, 2.f);
+    fill_rand_f<<<8, 256>>>(ss, q.B * 2 * q.cout, 24, 1.f);
+    fill_rand_f<<<1, 256>>>(bias, q.cout, 25, 1.f);
+    ConvArgs a{};
+    a.x1 = x; a.ld1 = q.cin; a.C1 = q.cin; a.Cin = q.cin; a.Hs = q.H; a.Ws = q.W; a.B = q.B; a.Ho = q.H; a.Wo = q.W;
+    a.Cout = q.cout; a.K = 9 * q.cin; a.w = w; a.y = y; a.ldy = q.cout; a.act = 1; a.bias = bias; a.zero = zero;
+    if (q.ss) { a.ss = ss; a.ss_ld = 2 * q.cout; }
+    if (q.res) { a.res1 = res; a.ldr1 = q.cout; }
+    std::vector<uint16_t> ref(npx * q.cout), got(npx * q.cout);
+    printf("%-26s", q.name);
+    for (int stg = 2; stg <= 4; ++stg) {
+      dac_c3i_st(stg);
+      dac_conv3_force(-1);
+      conv<bf16>(a, 3, 3, 1, 1, 0);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(stg == 2 ? ref.data() : got.data(), y, npx * q.cout * 2, hipMemcpyDeviceToHost));
+      bool same = stg == 2 || memcmp(ref.data(), got.data(), npx * q.cout * 2) == 0;
+      if (!same) ++bad;
+      hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) conv<bf16>(a, 3, 3, 1, 1, 0);
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("  ST%d %6.1f us%s", stg, ms * 1e3 / iters, same ? "" : " MISMATCH");
+    }
+    printf("\n");
+    dac_c3i_st(2);
+    CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(y)); CK(hipFree(res)); CK(hipFree(ss)); CK(hipFree(bias)); CK(hipFree(zero));
+  }
+  printf("c3i st: %s\n", bad ? "FAIL" : "OK (bit-identical)");
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "rbf")) {
     const int it = argc > 2 ? atoi(argv[2]) : 20;
     const int b = rbf_check<bf16>(it, "bf16");
