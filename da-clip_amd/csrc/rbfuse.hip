@@ -92,9 +92,13 @@ extern "C" void dac_rbfuse_enable(int on) { g_rbfuse_on = on; }
 // pair is MFMA-bound rather than HBM-bound — at B 8 the pair moves 3.5 TB/s, not the ~6 it would
 // need to be limited by HBM. Both forms are bit-identical, so this batch-dependent choice leaves
 // every image's output unchanged (tests/test_hip_parity.py batch tests).
+// In the network (rocprof, fp16 bench, B = 8) the 64 -> 64 fused block beats the pair too — 91.4
+// against 45.6 + 48.8 us, its cold-input reads cost the pair more than convbench's warm L2 shows —
+// while the Cin 128 form stays behind (153.1 against 91.4 + 48.8 us). So Cin 64 always, Cin 128 up
+// to two images.
 bool rbfuse_pays(const RbArgs& a) {
   const size_t px = (size_t)a.B * a.H * a.W, img = (size_t)256 * 256;
-  return g_rbfuse_on == 2 || px <= (a.Cin == 64 ? 4 : 2) * img;
+  return g_rbfuse_on == 2 || a.Cin == 64 || px <= 2 * img;
 }
 
 bool rbfuse_ok(const RbArgs& a) {
