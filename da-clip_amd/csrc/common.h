@@ -133,6 +133,20 @@ template <> struct Mma<float> {
   }
 };
 
+// Kernel arguments live in a fresh kernarg buffer per launch, so the first scalar load of every
+// 64-byte line of it misses the scalar cache. hipcc loads a struct argument's fields lazily, each
+// group behind its own s_waitcnt: a ConvArgs kernel paid five dependent misses (~1.2 us of its
+// prologue, tools/convbench_stamp). Touching every line once, up front, behind ONE wait turns the
+// later loads into hits.
+typedef const volatile __attribute__((address_space(4))) uint32_t kernarg_u32;
+template <int BYTES> DEV void kernarg_touch() {
+  kernarg_u32* p = (kernarg_u32*)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t acc = 0;
+#pragma unroll
+  for (int o = 0; o < BYTES; o += 64) acc ^= p[o / 4];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(acc) : "memory");
+}
+
 DEV float silu_f(float x) { return x / (1.f + expf(-x)); }
 DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 // Exact-form GELU 0.5 x (1 + erf(x / sqrt 2)) with erf from Abramowitz & Stegun 7.1.26

@@ -260,9 +260,13 @@ DEV void q8_store(const ConvArgs& a, size_t m, int nb, const float (&v)[16]) {
 // PRE: operands come from epi_prefetch and the conv has no bbias / res2 / (ss with res1) —
 // the epilogue then issues no loads at all, so it never waits for in-flight DMA.
 // Q8: the output is e4m3 + exponents (q8_store) instead of T.
-template <typename T, int TM, bool LN = false, bool PRE = false, bool Q8 = false, class PixOf>
+// PRE2 (with PRE): res1 rows in pre, res2 rows in pre2 (both loaded by the caller ahead of its K
+// loop, rows pix(i) of zero page when absent); bbias is still read here.
+template <typename T, int TM, bool LN = false, bool PRE = false, bool Q8 = false, bool PRE2 = false, class PixOf>
 DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&bi)[16], int nb, int b,
-                    const PixOf& pix, const EpiPref<TM>* pre = nullptr, const float* ssl = nullptr) {
+                    const PixOf& pix, const EpiPref<TM>* pre = nullptr, const float* ssl = nullptr,
+                    const EpiPref<TM>* pre2 = nullptr) {
+  static_assert(!PRE2 || PRE, "PRE2 extends PRE");
   T* y = reinterpret_cast<T*>(a.y);
   __builtin_amdgcn_sched_barrier(0);             // (not hoisted into the MFMA phase)
   if constexpr (PRE) {
@@ -271,6 +275,10 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
     // reused while its load is still in flight and then be overwritten when the load lands.
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(pre->v) / sizeof(pre->v[0])); ++k) asm volatile("" :: "v"(pre->v[k]));
+  }
+  if constexpr (PRE2) {
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(pre2->v) / sizeof(pre2->v[0])); ++k) asm volatile("" :: "v"(pre2->v[k]));
   }
   float sc[16], sh[16];
   if (a.ss && ssl) {                             // scale / shift rows staged in LDS by the caller
@@ -291,7 +299,7 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
     for (int e = 0; e < 16; ++e) { sc[e] = 1.f; sh[e] = 0.f; }
   }
   float bb[16];
-  if (!PRE && a.bbias) {
+  if ((!PRE || PRE2) && a.bbias) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) bb[e] = a.bbias[(size_t)b * a.bb_ld + nb + e];
   }
@@ -342,12 +350,13 @@ DEV void epi_regs16(const ConvArgs& a, const f32x4 (&acc)[TM][4], const float (&
 #pragma unroll
         for (int w = 0; w < 4; ++w) add_pair<T>(r1[w], v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
       }
-      if (!PRE && a.res2) {
-        const u32x4 r2 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res2) + m * a.ldr2 + nb + 8 * h);
+      if ((!PRE || PRE2) && a.res2) {
+        const u32x4 r2 = PRE2 ? pre2->v[2 * i + h]
+                              : *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(a.res2) + m * a.ldr2 + nb + 8 * h);
 #pragma unroll
         for (int w = 0; w < 4; ++w) add_pair<T>(r2[w], v[8 * h + 2 * w], v[8 * h + 2 * w + 1]);
       }
-      if (!PRE && a.bbias) {
+      if ((!PRE || PRE2) && a.bbias) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[8 * h + e] += bb[8 * h + e];
       }
@@ -415,6 +424,19 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int HWo = a.Ho * a.Wo;
+#ifdef DAC_STAMP
+  // Diagnostic build only (tools/convbench_stamp): per-block shader-clock stamps into a.part.
+  unsigned long long* stp = (!PART && a.part)
+      ? reinterpret_cast<unsigned long long*>(a.part) + (size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 8
+      : nullptr;
+#define DAC_ST(i, v) do { if (stp && tid == 0) stp[i] = (v); } while (0)
+#else
+#define DAC_ST(i, v) do { } while (0)
+#endif
+  DAC_ST(0, __builtin_amdgcn_s_memtime());
+  DAC_ST(1, __builtin_amdgcn_s_memrealtime());
+  kernarg_touch<sizeof(ConvArgs)>();
+  DAC_ST(7, __builtin_amdgcn_s_memtime());
   const TileId tl = xcd_tile();
   const bool batched = a.w_bstride > 0;
   const int M = batched ? (tl.bz + 1) * HWo : a.B * HWo;
@@ -435,11 +457,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     const int m = m0 + row;
     a_m[j] = m;
     if (m < M) {
-      const int b = m / HWo, r = m - b * HWo;
-      const int oh = r / a.Wo, ow = r - oh * a.Wo;
-      a_pix[j] = b * a.Hs * a.Ws;
-      a_ih[j] = oh * S - P;
-      a_iw[j] = ow * S - P;
+      if constexpr (KH == 1 && KW == 1 && S == 1 && P == 0) {
+        // Pointwise: row m reads pixel m; only its validity is needed (no divisions: the
+        // prologue's integer divisions were ~0.5 us of a 9 us GEMM, tools/convbench_stamp).
+        a_pix[j] = 0; a_ih[j] = 0; a_iw[j] = 0;
+      } else {
+        const int b = m / HWo, r = m - b * HWo;
+        const int oh = r / a.Wo, ow = r - oh * a.Wo;
+        a_pix[j] = b * a.Hs * a.Ws;
+        a_ih[j] = oh * S - P;
+        a_iw[j] = ow * S - P;
+      }
     } else {
       a_pix[j] = 0; a_ih[j] = -100000; a_iw[j] = -100000;
     }
@@ -588,6 +616,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
   for (int i = 0; i < (LNF ? TM : 1); ++i) ls1[i] = ls2[i] = lsh[i] = 0.f;
 
+  DAC_ST(6, __builtin_amdgcn_s_memtime());
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s);
   if constexpr (GNA) {
@@ -620,6 +649,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     }
   }
   const int lr = lane & 15, lg = lane >> 4;
+  // Swapped tiles: the epilogue's residual rows (res1, res2) are requested here, ahead of the K
+  // loop, by inline-asm loads the compiler's wait insertion cannot see; they land under the K
+  // loop instead of after it (the block's epilogue was 2.4 us warm / 5 us cold of a 9-15 us
+  // 512 -> 512 GEMM, tools/convbench_stamp). The loop's trailing vmcnt(0) covers them.
+  constexpr bool RPF = SWAP && !PART && !LNF && !GNA;
+  EpiPref<TM> rp1, rp2;
+  const bool rpf = RPF && (a.res1 || a.res2) && !a.ss;
+  if constexpr (RPF) {
+    if (rpf) {
+      const int nbr = n0 + wn * WTN + 16 * lg;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(rp1.v) / sizeof(rp1.v[0])); ++k) {
+        const int i = k / 2 < TM ? k / 2 : TM - 1, h = k & 1;
+        const size_t m = (size_t)m0 + wm * WTM + i * 16 + lr;
+        ld_asm(rp1.v[k], a.res1 ? (const void*)(reinterpret_cast<const T*>(a.res1) + m * a.ldr1 + nbr + 8 * h) : a.zero);
+        ld_asm(rp2.v[k], a.res2 ? (const void*)(reinterpret_cast<const T*>(a.res2) + m * a.ldr2 + nbr + 8 * h) : a.zero);
+      }
+    }
+  }
   for (int kt = 0; kt < nk; ++kt) {
     if constexpr (STAGES == 1) {
       // Single buffer (K fits one tile, or LDS kept small for occupancy): fill, wait, use.
@@ -637,6 +685,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
       asm volatile("" ::: "memory");
       issue(kt + STAGES - 1);                    // refills the slot read at iteration kt-1
     }
+    if (kt == 0) DAC_ST(2, __builtin_amdgcn_s_memtime());
     const char* A = smem + (kt % STAGES) * STAGE;
     const char* Bs = A + BM * 128;
 #pragma unroll
@@ -695,6 +744,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  DAC_ST(3, __builtin_amdgcn_s_memtime());
   if constexpr (LNF) {
     // Row moments -> acc = rstd * (acc - mean * cs[n]), the LN'd-input GEMM before its bias.
     const float inv_n = 1.f / (float)a.lnf_n;
@@ -740,10 +790,25 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     float bi[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
-    epi_regs16<T, TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+    if constexpr (RPF && !SLN) {
+      if (rpf) {
+        epi_regs16<T, TM, false, true, false, true>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; },
+                                                    &rp1, nullptr, &rp2);
+      } else {
+        epi_regs16<T, TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+      }
+    } else {
+      epi_regs16<T, TM, SLN>(a, acc, bi, nb, bimg, [&](int i) { return (size_t)m0 + wm * WTM + i * 16 + lr; });
+    }
   } else {
     conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPE>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
   }
+#ifdef DAC_STAMP
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  DAC_ST(4, __builtin_amdgcn_s_memtime());
+  DAC_ST(5, __builtin_amdgcn_s_memrealtime());
+#undef DAC_ST
 }
 
 

@@ -1002,6 +1002,74 @@ template <typename E> static int rbf_check(int iters, const char* tn) {
 }
 
 extern "C" void dac_c3i_st(int v);
+#ifdef DAC_STAMP
+// Per-block shader-clock stamps of the 1x1 GEMM kernel (build: make convbench_stamp): where one
+// launch's time goes -- first data landed, K loop, epilogue -- with warm and with flushed caches.
+static int stamp_check() {
+  struct Q { const char* name; int cin, cout, res; };
+  const Q shapes[] = {{"1x1 512->512 +r", 512, 512, 1}, {"1x1 2048->512 +r", 2048, 512, 1}, {"1x1 256->256", 256, 256, 0},
+                      {"1x1 512->1536", 512, 1536, 0}};
+  const int B = 8, H = 32, W = 32;
+  const size_t npx = (size_t)B * H * W, big = (size_t)1 << 29;
+  void* flush; CK(hipMalloc(&flush, big));
+  for (const Q& q : shapes) {
+    bf16 *x, *w, *y, *res; float* bias; void* zero; unsigned long long* st;
+    CK(hipMalloc(&x, npx * q.cin * 2)); CK(hipMalloc(&w, (size_t)q.cout * q.cin * 2)); CK(hipMalloc(&y, npx * q.cout * 2));
+    CK(hipMalloc(&res, npx * q.cout * 2)); CK(hipMalloc(&bias, q.cout * 4)); CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+    fill_rand<<<(npx * q.cin + 255) / 256, 256>>>(x, npx * q.cin, 31, 2.f);
+    fill_rand<<<((size_t)q.cout * q.cin + 255) / 256, 256>>>(w, (size_t)q.cout * q.cin, 32, 0.1f);
+    fill_rand<<<(npx * q.cout + 255) / 256, 256>>>(res, npx * q.cout, 33, 2.f);
+    fill_rand_f<<<4, 256>>>(bias, q.cout, 34, 1.f);
+    const int nblk = 65536;
+    CK(hipMalloc(&st, (size_t)nblk * 8 * 8));
+    ConvArgs a{};
+    a.x1 = x; a.ld1 = q.cin; a.C1 = q.cin; a.Cin = q.cin; a.Hs = H; a.Ws = W; a.B = B; a.Ho = H; a.Wo = W;
+    a.Cout = q.cout; a.K = q.cin; a.w = w; a.y = y; a.ldy = q.cout; a.bias = bias; a.zero = zero;
+    if (q.res) { a.res1 = res; a.ldr1 = q.cout; }
+    for (int cold = 0; cold < 2; ++cold) {
+      a.part = nullptr;
+      for (int i = 0; i < 3; ++i) conv<bf16>(a, 1, 1, 1, 0, 0);
+      if (cold) CK(hipMemsetAsync(flush, cold, big, 0));
+      CK(hipMemset(st, 0, (size_t)nblk * 64));
+      CK(hipDeviceSynchronize());
+      a.part = reinterpret_cast<float*>(st);
+      hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+      if (cold) CK(hipMemsetAsync(flush, 2, big, 0));
+      CK(hipEventRecord(e0, 0));
+      conv<bf16>(a, 1, 1, 1, 0, 0);
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      std::vector<unsigned long long> h((size_t)nblk * 8);
+      CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+      // s_memtime counts shader clocks of the block's own XCD (counters differ between XCDs), so
+      // each block converts its intervals with its own clock: (t4 - t0) / (realtime span).
+      unsigned long long r0 = ~0ull, r5 = 0;
+      double first = 0, loop = 0, epi = 0, tot = 0, clk = 0, st0 = 0, setup = 0, karg = 0; int n = 0;
+      for (int b = 0; b < nblk; ++b) {
+        const unsigned long long* p = &h[(size_t)b * 8];
+        if (!p[0] || !p[4] || p[5] <= p[1]) continue;
+        ++n;
+        r0 = std::min(r0, p[1]); r5 = std::max(r5, p[5]);
+        const double rt = (double)(p[5] - p[1]) / 100.0;             // this block's life, us (100 MHz)
+        const double c = (double)(p[4] - p[0]) / rt;                 // its clock, cycles per us
+        clk += c; tot += rt;
+        setup += (double)(p[6] - p[0]) / c; karg += (double)(p[7] - p[0]) / c;
+        first += (double)(p[2] - p[6]) / c; loop += (double)(p[3] - p[2]) / c; epi += (double)(p[4] - p[3]) / c;
+      }
+      for (int b = 0; b < nblk; ++b) {
+        const unsigned long long* p = &h[(size_t)b * 8];
+        if (!p[0] || !p[4] || p[5] <= p[1]) continue;
+        st0 += (double)(p[1] - r0) / 100.0;                           // start offset after the first block
+      }
+      const double us_rt = (double)(r5 - r0) / 100.0;
+      printf("%-18s %s  event %6.1f us  span %6.1f us  blocks %d  clk %.2f GHz  per block: life %5.2f us (start +%5.2f)  kernarg %5.2f setup %5.2f  first data %5.2f  K loop %5.2f  epilogue %5.2f us\n",
+             q.name, cold ? "cold" : "warm", ms * 1e3, us_rt, n, clk / n / 1e3, tot / n, st0 / n, karg / n, setup / n, first / n, loop / n, epi / n);
+    }
+    CK(hipFree(x)); CK(hipFree(w)); CK(hipFree(y)); CK(hipFree(res)); CK(hipFree(bias)); CK(hipFree(zero)); CK(hipFree(st));
+  }
+  return 0;
+}
+#endif
 // Small-grid v4 ring depth (DAC_C3I_ST): time ST = 2 / 3 / 4 on the one-block-per-CU 3x3 shapes and
 // require bit-identical outputs (the stage count only buffers the same ordered sum).
 static int c3i_st_check(int iters) {
@@ -1056,6 +1124,9 @@ static int c3i_st_check(int iters) {
 
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
+#ifdef DAC_STAMP
+  if (argc > 1 && !strcmp(argv[1], "stamp")) return stamp_check();
+#endif
   if (argc > 1 && !strcmp(argv[1], "rbf")) {
     const int it = argc > 2 ? atoi(argv[2]) : 20;
     const int b = rbf_check<bf16>(it, "bf16");
