@@ -16,6 +16,10 @@ int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 int g_conv3h_on = getenv("DAC_CONV3H") ? atoi(getenv("DAC_CONV3H")) : 0;
 int g_c3i_st = getenv("DAC_C3I_ST") ? atoi(getenv("DAC_C3I_ST")) : 3;
 extern "C" void dac_c3i_st(int v) { g_c3i_st = v; }
+// GEGLU projections on swapped tiles with the register epilogue: 0 off (the 256x256 LDS-epilogue
+// tile), 1 256x256 (16 waves), 2 128x256, 3 256x128, 4 128x128 (DAC_GEGLU_SW; convbench forces
+// 20..23 = configurations 1..4).
+int g_geglu_sw = getenv("DAC_GEGLU_SW") ? atoi(getenv("DAC_GEGLU_SW")) : 1;
 extern "C" void dac_conv3_force(int v) { g_conv3_force = v; }
 extern "C" void dac_conv2_force(int v) { g_conv2_force = v; }
 

@@ -411,8 +411,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   static_assert(!GNA || (KH == 1 && KW == 1 && sizeof(T) == 2 && (EPE & EPI_SWAP) && !LNF), "GN in A: 16-bit 1x1 swapped");
   constexpr bool SWAP = (EPE & EPI_SWAP) != 0;
   constexpr bool SLN = (EPE & EPI_LN) != 0 && SWAP;
-  static_assert(!SWAP || ((EPE == EPI_SWAP || (EPE == (EPI_SWAP | EPI_LN) && WGN == 1 && BN == 64)) && TN == 4 &&
-                          sizeof(T) == 2), "swapped tiles");
+  // EPI_SWAP | EPI_GEGLU: weights in the swapped GEGLU order (ConvArgs::w_gs), register epilogue.
+  constexpr bool SGEGLU = EPE == (EPI_SWAP | EPI_GEGLU);
+  static_assert(!SWAP || ((EPE == EPI_SWAP || SGEGLU || (EPE == (EPI_SWAP | EPI_LN) && WGN == 1 && BN == 64)) &&
+                          TN == 4 && sizeof(T) == 2), "swapped tiles");
   constexpr int PIPE = STAGES * STAGE;
   constexpr int EPR = epi_rows<BM, BN, WTM>(PIPE);
   // (scale, shift) x Cin <= 512, (mean, rstd) x 64 groups: 4.5 KB, so three 64x128 blocks still
@@ -653,7 +655,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   // loop, by inline-asm loads the compiler's wait insertion cannot see; they land under the K
   // loop instead of after it (the block's epilogue was 2.4 us warm / 5 us cold of a 9-15 us
   // 512 -> 512 GEMM, tools/convbench_stamp). The loop's trailing vmcnt(0) covers them.
-  constexpr bool RPF = SWAP && !PART && !LNF && !GNA;
+  constexpr bool RPF = SWAP && !PART && !LNF && !GNA && !SGEGLU;
   EpiPref<TM> rp1, rp2;
   const bool rpf = RPF && (a.res1 || a.res2) && !a.ss;
   if constexpr (RPF) {
@@ -784,7 +786,26 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   }
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  if constexpr (SWAP) {
+  if constexpr (SGEGLU) {
+    // Lane (lr, lg), pixel row i: x of output channels ob .. ob + 7 in acc elements 0..7, their
+    // gate in 8..15 (w_gs order); (x + bx) * gelu(gate + bg), the LDS epilogue's formula, stored
+    // as 16 bytes. The dispatcher guarantees whole tiles inside one image and Cout % BN == 0.
+    const int nb = n0 + wn * WTN + 16 * lg, ob = nb / 2;
+    float bi[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) bi[e] = a.bias ? a.bias[nb + e] : 0.f;
+    T* y = reinterpret_cast<T*>(a.y);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const size_t m = (size_t)m0 + wm * WTM + i * 16 + lr;
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        o[c] = (acc[i][c >> 2][c & 3] + bi[c]) * gelu_fast(acc[i][(8 + c) >> 2][(8 + c) & 3] + bi[8 + c]);
+      store_vec<T>(y + m * a.ldy + ob, o);
+    }
+  } else if constexpr (SWAP) {
     // The dispatcher guarantees whole tiles inside one image and Cout % BN == 0.
     const int nb = n0 + wn * WTN + 16 * lg;
     float bi[16];
@@ -1506,6 +1527,7 @@ extern int g_conv3h_on;       // v6 2-D halo kernel: 0 off, 1 measured-faster sh
 // 256->256 21.6 -> 18.9 us, 64x64 128->128 18.2 -> 17.6 us in the network, +0.45 % images/s). The stage count only
 // buffers: every output is the same ordered sum, so the choice leaves results bit-identical.
 extern int g_c3i_st;
+extern int g_geglu_sw;
 inline int c3i_small_st(const ConvArgs& a, int BM) {
   const long tiles = (long)a.B * a.Ho * a.Wo / BM * ((a.Cout + 63) / 64);
   return tiles <= 256 ? g_c3i_st : 2;
@@ -2415,6 +2437,30 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
       // general one spills at this tile); the rest 64x128 with 2 stages (4 waves of 32x64),
       // which doubles the blocks of the small 32x32-level GEMMs over 128x128.
       if (a.act == ACT_GEGLU) {
+        // Swapped tiles with the register GEGLU epilogue (weights in the w_gs order): no LDS
+        // staging of the fp32 tile, 16-byte stores straight from the accumulators.
+        if constexpr (sizeof(T) == 2)
+          if (a.w_gs && a.b_gs && rows_ok && !a.res1 && !a.res2 && !a.bbias && !a.ss && g_geglu_sw > 0) {
+            ConvArgs q = a;
+            q.w = a.w_gs; q.bias = a.b_gs;
+            const int cfg = g_conv2_force >= 20 && g_conv2_force <= 23 ? g_conv2_force - 19 : g_geglu_sw;
+            if (cfg == 1 && (batched || HWo % 256 == 0) && a.Cout % 256 == 0) {
+              conv2_kernel<T, 256, 256, 4, 4, 2, KH, KW, S, P, EPI_SWAP | EPI_GEGLU><<<dim3((Mg + 255) / 256, a.Cout / 256, gz), 1024, 0, st>>>(q);
+              return;
+            }
+            if (cfg == 2 && (batched || HWo % 128 == 0) && a.Cout % 256 == 0) {
+              conv2_kernel<T, 128, 256, 2, 4, 2, KH, KW, S, P, EPI_SWAP | EPI_GEGLU><<<dim3((Mg + 127) / 128, a.Cout / 256, gz), 512, 0, st>>>(q);
+              return;
+            }
+            if (cfg == 3 && (batched || HWo % 256 == 0) && a.Cout % 128 == 0) {
+              conv2_kernel<T, 256, 128, 4, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_GEGLU><<<dim3((Mg + 255) / 256, a.Cout / 128, gz), 512, 0, st>>>(q);
+              return;
+            }
+            if (cfg == 4 && (batched || HWo % 128 == 0) && a.Cout % 128 == 0) {
+              conv2_kernel<T, 128, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_GEGLU><<<dim3((Mg + 127) / 128, a.Cout / 128, gz), 256, 0, st>>>(q);
+              return;
+            }
+          }
         // 256x256 tiles when they stay inside one image: half the LDS-DMA bytes per MFMA of
         // the 128x256 tiles, whose per-stage refill the MFMAs could not cover.
         if constexpr (sizeof(T) == 2)

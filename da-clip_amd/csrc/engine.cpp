@@ -515,6 +515,20 @@ struct Packer {
     cw.w = upload_T(p, key);
     make_fp8(cw, p, 2 * F, I);
     cw.b = (const float*)pool.upload(pb.data(), pb.size() * 4);
+    if (sizeof(T) == 2 && F % 32 == 0) {
+      // Swapped-tile order (ConvArgs::w_gs): row L of 64-row group G = L / 64, lane group
+      // lg = (L % 64) / 16, e = L % 16 is x (e < 8) or gate (e >= 8) of output channel
+      // 32 G + 8 lg + (e & 7).
+      std::vector<float> q((size_t)2 * F * I), qb(2 * F);
+      for (int L = 0; L < 2 * F; ++L) {
+        const int G = L / 64, lg = (L % 64) / 16, e = L % 16;
+        const int src = (e < 8 ? 0 : F) + 32 * G + 8 * lg + (e & 7);
+        std::copy(w->v.begin() + (size_t)src * I, w->v.begin() + (size_t)(src + 1) * I, q.begin() + (size_t)L * I);
+        qb[L] = b->v[src];
+      }
+      cw.w_gs = upload_T(q, key);
+      cw.b_gs = (const float*)pool.upload(qb.data(), qb.size() * 4);
+    }
     if (keep) *keep = std::move(p);
     if (keep_b) *keep_b = std::move(pb);
     return cw;
@@ -555,6 +569,7 @@ static ConvArgs conv_args(const Run& r, const ConvW& cw, const void* x1, int ld1
   a.gna_stats = e.gna_stats; a.gna_g = e.gna_g; a.gna_b = e.gna_b; a.gna_groups = e.gna_groups;
   a.gna_nb = e.gna_nb; a.gna_eps = e.gna_eps;
   a.ys8 = e.ys8; a.xs8 = e.xs8;
+  if (e.act == ACT_GEGLU) { a.w_gs = cw.w_gs; a.b_gs = cw.b_gs; }
   if (e.fuse1x1) {
     a.w2 = e.fuse1x1->w; a.w2_dual = e.fuse1x1->dual; a.bias2 = e.fuse1x1->b; a.y2 = e.y2; a.ldy2 = e.ldy2;
   }

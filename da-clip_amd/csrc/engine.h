@@ -72,6 +72,10 @@ struct ConvW {
   // exponents [64][9][2] (per output channel, tap, 32-channel half) for conv3q.hip.
   const uint8_t* q8w = nullptr;
   const uint8_t* q8s = nullptr;
+  // GEGLU projections, 16-bit handles: the weights / bias again in the swapped-tile order
+  // (ConvArgs::w_gs, b_gs).
+  const void* w_gs = nullptr;
+  const float* b_gs = nullptr;
   // 16-bit handles, 3x3 convs over a 2x nearest-upsampled input: row-phase weights
   // [cout][4][3][cin] = (W0, W1+W2 | W0+W1, W2) (ConvArgs::uph).
   const void* wph = nullptr;

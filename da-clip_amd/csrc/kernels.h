@@ -100,6 +100,13 @@ struct ConvArgs {
   // applies the epilogue (bias, activation, residuals) — set by the engine with the workspace.
   int ksplit;
   float* part;
+  // GEGLU projections (attention.py:37-64), 16-bit: the same weights in the swapped-tile order
+  // (w_gs, bias b_gs): in each 64-row group G, rows 16 lg + e hold the x rows (e < 8) and the gate
+  // rows (e >= 8) of output channels 32 G + 8 lg + (e & 7), so a swapped tile's lane ends with x
+  // and gate of 8 consecutive output channels of one pixel (register epilogue, 16-byte stores).
+  // Null: only the 16-row-interleaved order in w / bias exists.
+  const void* w_gs;
+  const float* b_gs;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);

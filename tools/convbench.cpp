@@ -1002,13 +1002,83 @@ template <typename E> static int rbf_check(int iters, const char* tn) {
 }
 
 extern "C" void dac_c3i_st(int v);
+// GEGLU projections on swapped tiles (ConvArgs::w_gs) against the 16-row-interleaved LDS-epilogue
+// tile: the same reference weights in both orders; outputs compared element by element (max
+// |diff| / max |ref|) and both forms timed (configurations 20..23 = DAC_GEGLU_SW 1..4).
+static int gsw_check(int iters) {
+  struct Q { const char* name; int cin, F; };
+  const Q shapes[] = {{"geglu 512->2x2048", 512, 2048}, {"geglu 256->2x1024", 256, 1024}};
+  const int B = 8, H = 32, W = 32;
+  const size_t npx = (size_t)B * H * W;
+  int bad = 0;
+  for (const Q& q : shapes) {
+    const int F = q.F, I = q.cin;
+    std::vector<float> wr((size_t)2 * F * I), br(2 * F);
+    uint32_t st = 777u;
+    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return ((st >> 8) / 16777216.f - 0.5f); };
+    for (auto& v : wr) v = 0.2f * rnd();
+    for (auto& v : br) v = rnd();
+    std::vector<bf16> wo((size_t)2 * F * I), wg((size_t)2 * F * I);
+    std::vector<float> bo(2 * F), bg(2 * F);
+    for (int r = 0; r < 2 * F; ++r) {
+      const int g = r / 32, s2 = r % 32, so = s2 < 16 ? 16 * g + s2 : F + 16 * g + (s2 - 16);
+      const int G = r / 64, lg = (r % 64) / 16, e = r % 16, sg = (e < 8 ? 0 : F) + 32 * G + 8 * lg + (e & 7);
+      for (int k = 0; k < I; ++k) { wo[(size_t)r * I + k] = (bf16)wr[(size_t)so * I + k]; wg[(size_t)r * I + k] = (bf16)wr[(size_t)sg * I + k]; }
+      bo[r] = br[so]; bg[r] = br[sg];
+    }
+    bf16 *x, *dwo, *dwg, *y; float *dbo, *dbg; void* zero;
+    CK(hipMalloc(&x, npx * I * 2)); CK(hipMalloc(&dwo, wo.size() * 2)); CK(hipMalloc(&dwg, wg.size() * 2));
+    CK(hipMalloc(&y, npx * F * 2)); CK(hipMalloc(&dbo, bo.size() * 4)); CK(hipMalloc(&dbg, bg.size() * 4));
+    CK(hipMalloc(&zero, 256)); CK(hipMemset(zero, 0, 256));
+    fill_rand<<<(npx * I + 255) / 256, 256>>>(x, npx * I, 41, 2.f);
+    CK(hipMemcpy(dwo, wo.data(), wo.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dwg, wg.data(), wg.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dbo, bo.data(), bo.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dbg, bg.data(), bg.size() * 4, hipMemcpyHostToDevice));
+    ConvArgs a{};
+    a.x1 = x; a.ld1 = I; a.C1 = I; a.Cin = I; a.Hs = H; a.Ws = W; a.B = B; a.Ho = H; a.Wo = W;
+    a.Cout = 2 * F; a.K = I; a.w = dwo; a.bias = dbo; a.y = y; a.ldy = F; a.act = 3; a.zero = zero;
+    std::vector<bf16> ref(npx * F), got(npx * F);
+    auto time_it = [&]() {
+      hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+      conv<bf16>(a, 1, 1, 1, 0, 0);
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) conv<bf16>(a, 1, 1, 1, 0, 0);
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      return ms * 1e3 / iters;
+    };
+    dac_conv2_force(0);
+    a.w_gs = nullptr; a.b_gs = nullptr;
+    const double t0 = time_it();
+    CK(hipMemcpy(ref.data(), y, ref.size() * 2, hipMemcpyDeviceToHost));
+    printf("%-20s LDS-epilogue tile %6.1f us", q.name, t0);
+    a.w_gs = dwg; a.b_gs = dbg;
+    for (int f = 20; f <= 23; ++f) {
+      dac_conv2_force(f);
+      CK(hipMemset(y, 0, npx * F * 2));
+      const double t = time_it();
+      CK(hipMemcpy(got.data(), y, got.size() * 2, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (size_t i = 0; i < ref.size(); ++i) { md = fmax(md, fabs((double)(float)got[i] - (float)ref[i])); mx = fmax(mx, fabs((double)(float)ref[i])); }
+      const bool ok = md <= 1e-2 * mx;
+      if (!ok) ++bad;
+      printf("  | sw%d %6.1f us rel %.1e%s", f - 19, t, mx > 0 ? md / mx : 0.0, ok ? "" : " FAIL");
+    }
+    dac_conv2_force(0);
+    printf("\n");
+    CK(hipFree(x)); CK(hipFree(dwo)); CK(hipFree(dwg)); CK(hipFree(y)); CK(hipFree(dbo)); CK(hipFree(dbg)); CK(hipFree(zero));
+  }
+  printf("gsw: %s\n", bad ? "FAIL" : "OK");
+  return bad ? 1 : 0;
+}
 #ifdef DAC_STAMP
 // Per-block shader-clock stamps of the 1x1 GEMM kernel (build: make convbench_stamp): where one
 // launch's time goes -- first data landed, K loop, epilogue -- with warm and with flushed caches.
 static int stamp_check() {
-  struct Q { const char* name; int cin, cout, res; };
-  const Q shapes[] = {{"1x1 512->512 +r", 512, 512, 1}, {"1x1 2048->512 +r", 2048, 512, 1}, {"1x1 256->256", 256, 256, 0},
-                      {"1x1 512->1536", 512, 1536, 0}};
+  struct Q { const char* name; int cin, cout, res, geglu; };
+  const Q shapes[] = {{"1x1 512->512 +r", 512, 512, 1, 0}, {"1x1 2048->512 +r", 2048, 512, 1, 0}, {"1x1 256->256", 256, 256, 0, 0},
+                      {"1x1 512->1536", 512, 1536, 0, 0}, {"1x1 512->4096 geglu", 512, 4096, 0, 1}};
   const int B = 8, H = 32, W = 32;
   const size_t npx = (size_t)B * H * W, big = (size_t)1 << 29;
   void* flush; CK(hipMalloc(&flush, big));
@@ -1024,7 +1094,8 @@ static int stamp_check() {
     CK(hipMalloc(&st, (size_t)nblk * 8 * 8));
     ConvArgs a{};
     a.x1 = x; a.ld1 = q.cin; a.C1 = q.cin; a.Cin = q.cin; a.Hs = H; a.Ws = W; a.B = B; a.Ho = H; a.Wo = W;
-    a.Cout = q.cout; a.K = q.cin; a.w = w; a.y = y; a.ldy = q.cout; a.bias = bias; a.zero = zero;
+    a.Cout = q.cout; a.K = q.cin; a.w = w; a.y = y; a.ldy = q.geglu ? q.cout / 2 : q.cout; a.bias = bias; a.zero = zero;
+    if (q.geglu) a.act = 3;
     if (q.res) { a.res1 = res; a.ldr1 = q.cout; }
     for (int cold = 0; cold < 2; ++cold) {
       a.part = nullptr;
@@ -1124,6 +1195,7 @@ static int c3i_st_check(int iters) {
 
 int main(int argc, char** argv) {
   if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
+  if (argc > 1 && !strcmp(argv[1], "gsw")) return gsw_check(argc > 2 ? atoi(argv[2]) : 20);
 #ifdef DAC_STAMP
   if (argc > 1 && !strcmp(argv[1], "stamp")) return stamp_check();
 #endif
