@@ -1303,28 +1303,12 @@ struct UNetNet {
     return n + (s - n % s) % s;
   }
 
-  // One forward. ss: [B][ss_total] of this step; out: [B*Hp*Wp][ldo] (channels < out_nc).
-  void forward(Run& r, const float* xt, const float* mu, int B, int H, int W, const float* ss,
-               const float* cc, void* out, int ldo) {
-    const int Hp = pad_of(H), Wp = pad_of(W);
-    const size_t M0 = (size_t)B * Hp * Wp;
-    T* xin = r.alloc<T>(M0 * 8);
-    if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
-    T* x0 = r.alloc<T>(M0 * nf);
-    // Roles are assigned per section below; this scope restores the caller's role when the
-    // forward returns (ViT / encoder calls on the thread are unaffected).
-    RoleScope rs_init(R_INIT);
-    conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
+  // Levels sl .. depth-1 for images [0, B) of the pointers given: downs[sl..] (their skips stay
+  // inside), the middle blocks, ups[..depth-1-sl], the last sampling conv writing yout
+  // (B x (2h x 2w) x Cin of level sl; same resolution when sl == 0).
+  void section(Run& r, int sl, const void* cur, int B, int h, int w, const float* ss, const float* cc, T* yout) {
     std::vector<std::pair<const void*, int>> hs;
-    const void* cur = x0;
-    int h = Hp, w = Wp;
-    if (half) {                                   // Wild-IR: levels run at half resolution
-      T* xd = r.alloc<T>((size_t)B * (Hp / 2) * (Wp / 2) * nf);
-      conv_call<T>(r, half_down, x0, nf, nf, nullptr, 0, B, Hp, Wp, 0, 2, 1, xd, nf, Epi());
-      cur = xd;
-      h = Hp / 2; w = Wp / 2;
-    }
-    for (int i = 0; i < depth; ++i) {
+    for (int i = sl; i < depth; ++i) {
       const auto [din, dout] = levels[i];
       Level& L = downs[i];
       g_role = R_RB;
@@ -1350,7 +1334,123 @@ struct UNetNet {
     cur = resblock(r, mid1, cur, mid, nullptr, 0, B, h, w, ss);
     cur = attn(r, mid_attn, cur, mid, B, h, w, cc);
     cur = resblock(r, mid2, cur, mid, nullptr, 0, B, h, w, ss);
-    for (int j = 0; j < depth; ++j) {
+    for (int j = 0; j < depth - sl; ++j) {
+      const int i = depth - 1 - j;
+      const auto [din, dout] = levels[i];
+      Level& L = ups[j];
+      auto sk = hs.back(); hs.pop_back();
+      g_role = R_RB;
+      cur = resblock(r, L.b1, cur, dout, sk.first, sk.second, B, h, w, ss);
+      sk = hs.back(); hs.pop_back();
+      cur = resblock(r, L.b2, cur, dout, sk.first, sk.second, B, h, w, ss);
+      cur = attn(r, L.at, cur, dout, B, h, w, cc);
+      g_role = R_SAMP;
+      const bool last = j == depth - 1 - sl;
+      if (i != 0) {
+        T* y = last ? yout : r.alloc<T>((size_t)B * (2 * h) * (2 * w) * din);
+        conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 1, 1, 1, y, din, Epi());
+        h *= 2; w *= 2;
+        cur = y;
+      } else {
+        T* y = last ? yout : r.alloc<T>((size_t)B * h * w * din);
+        conv_call<T>(r, L.samp, cur, dout, dout, nullptr, 0, B, h, w, 0, 1, 1, y, din, Epi());
+        cur = y;
+      }
+    }
+  }
+
+  // One forward. ss: [B][ss_total] of this step; out: [B*Hp*Wp][ldo] (channels < out_nc).
+  void forward(Run& r, const float* xt, const float* mu, int B, int H, int W, const float* ss,
+               const float* cc, void* out, int ldo) {
+    const int Hp = pad_of(H), Wp = pad_of(W);
+    const size_t M0 = (size_t)B * Hp * Wp;
+    T* xin = r.alloc<T>(M0 * 8);
+    if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
+    T* x0 = r.alloc<T>(M0 * nf);
+    // Roles are assigned per section below; this scope restores the caller's role when the
+    // forward returns (ViT / encoder calls on the thread are unaffected).
+    RoleScope rs_init(R_INIT);
+    conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
+    std::vector<std::pair<const void*, int>> hs;
+    const void* cur = x0;
+    int h = Hp, w = Wp;
+    if (half) {                                   // Wild-IR: levels run at half resolution
+      T* xd = r.alloc<T>((size_t)B * (Hp / 2) * (Wp / 2) * nf);
+      conv_call<T>(r, half_down, x0, nf, nf, nullptr, 0, B, Hp, Wp, 0, 2, 1, xd, nf, Epi());
+      cur = xd;
+      h = Hp / 2; w = Wp / 2;
+    }
+    // Section split (DAC_SPLIT_LVL: first level of the section, counted from the bottom, 0 = off;
+    // DAC_SPLIT_N: branches).
+    static const int split_lvl = getenv("DAC_SPLIT_LVL") ? atoi(getenv("DAC_SPLIT_LVL")) : 1;
+    static const int split_n = getenv("DAC_SPLIT_N") ? atoi(getenv("DAC_SPLIT_N")) : 2;
+    const int nbr = std::min({split_n, B, 1 + Run::kSide});
+    const bool split = split_lvl > 0 && nbr >= 2 && r.side[nbr - 2];
+    const int sl = split ? std::max(0, depth - split_lvl) : depth;
+    for (int i = 0; i < sl; ++i) {
+      const auto [din, dout] = levels[i];
+      Level& L = downs[i];
+      g_role = R_RB;
+      cur = resblock(r, L.b1, cur, din, nullptr, 0, B, h, w, ss);
+      hs.push_back({cur, din});
+      cur = resblock(r, L.b2, cur, din, nullptr, 0, B, h, w, ss);
+      cur = attn(r, L.at, cur, din, B, h, w, cc);
+      g_role = R_SAMP;
+      hs.push_back({cur, din});
+      if (i != depth - 1) {
+        T* y = r.alloc<T>((size_t)B * (h / 2) * (w / 2) * dout);
+        conv_call<T>(r, L.samp, cur, din, din, nullptr, 0, B, h, w, 0, 2, 1, y, dout, Epi());
+        h /= 2; w /= 2;
+        cur = y;
+      } else {
+        T* y = r.alloc<T>((size_t)B * h * w * dout);
+        conv_call<T>(r, L.samp, cur, din, din, nullptr, 0, B, h, w, 0, 1, 1, y, dout, Epi());
+        cur = y;
+      }
+    }
+    if (!split) {
+      const int mid = levels.back().second;
+      g_role = R_MID;
+      cur = resblock(r, mid1, cur, mid, nullptr, 0, B, h, w, ss);
+      cur = attn(r, mid_attn, cur, mid, B, h, w, cc);
+      cur = resblock(r, mid2, cur, mid, nullptr, 0, B, h, w, ss);
+    } else {
+      // The lowest split_lvl levels (the 32x32 level at 256^2 by default: downs[depth-1], the
+      // middle blocks, ups[0]) have small, latency-bound kernels, so with B >= 2
+      // they run as nbr concurrent branches of B / nbr images (streams r.st + r.side) whose
+      // prologues, epilogues and tails overlap. Every kernel is per-image (batch-invariant): the
+      // outputs are bit-identical to one full-batch branch. Output: the section's last sampling
+      // conv, all images.
+      const int C0 = levels[sl].first;
+      const int h0 = h, w0 = w;
+      const size_t px = (size_t)h * w;
+      if (sl != 0) { h *= 2; w *= 2; }
+      const size_t pxo = (size_t)h * w;
+      T* y = r.alloc<T>((size_t)B * pxo * C0);
+      if (!r.dry) {
+        HIP_OK(hipEventRecord(r.evf, r.st));
+        for (int k = 0; k + 1 < nbr; ++k) HIP_OK(hipStreamWaitEvent(r.side[k], r.evf, 0));
+      }
+      double fl = 0;
+      for (int k = 0; k < nbr; ++k) {
+        const int b0 = (int)((long)B * k / nbr), b1 = (int)((long)B * (k + 1) / nbr);
+        Run rk = r;
+        rk.st = k ? r.side[k - 1] : r.st;
+        rk.flops = 0;
+        section(rk, sl, static_cast<const T*>(cur) + b0 * px * C0, b1 - b0, h0, w0,
+                ss ? ss + (size_t)b0 * ss_total : nullptr, cc ? cc + (size_t)b0 * cc_total : nullptr,
+                y + b0 * pxo * C0);
+        fl += rk.flops;
+      }
+      r.flops += fl;
+      if (!r.dry)
+        for (int k = 0; k + 1 < nbr; ++k) {
+          HIP_OK(hipEventRecord(r.evj[k], r.side[k]));
+          HIP_OK(hipStreamWaitEvent(r.st, r.evj[k], 0));
+        }
+      cur = y;
+    }
+    for (int j = depth - sl; j < depth; ++j) {
       const int i = depth - 1 - j;
       const auto [din, dout] = levels[i];
       Level& L = ups[j];
@@ -1593,6 +1693,11 @@ class EngineT : public Engine {
   EngineT(int device, const dac_config& c, bool fp8w = false) : dev(device), cfg(c), fp8(fp8w) {
     HIP_OK(hipSetDevice(dev));
     HIP_OK(hipStreamCreateWithFlags(&priv, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    for (int k = 0; k < Run::kSide; ++k) {
+      HIP_OK(hipStreamCreateWithFlags(&side[k], hipStreamNonBlocking));
+      HIP_OK(hipEventCreateWithFlags(&ev_join[k], hipEventDisableTiming));
+    }
     HIP_OK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
     zero_page = pool.alloc(256);
@@ -1615,6 +1720,11 @@ class EngineT : public Engine {
     for (auto& kv : bufs) free_bufs(kv.second);
     (void)hipEventDestroy(ev_in);
     (void)hipEventDestroy(ev_out);
+    (void)hipEventDestroy(ev_fork);
+    for (int k = 0; k < Run::kSide; ++k) {
+      (void)hipEventDestroy(ev_join[k]);
+      (void)hipStreamDestroy(side[k]);
+    }
     (void)hipStreamDestroy(priv);
   }
 
@@ -1711,12 +1821,17 @@ class EngineT : public Engine {
     Run r;
     r.dry = true;
     r.ar = &a;
+    set_side(r);       // same allocation sequence as the live (split) forward
     const float* dummy = (const float*)1;
     unet->tables(r, nullptr, nT, 0.0, 0.0, 1.0, dummy, has_ic ? dummy : nullptr, B, nullptr, nullptr);
     const size_t t = a.peak;
     a.reset();
     unet->forward(r, nullptr, nullptr, B, H, W, nullptr, has_ic ? dummy : nullptr, nullptr, 4);
     return std::max(t, a.peak) + (1 << 20);
+  }
+  void set_side(Run& r) {
+    for (int k = 0; k < Run::kSide; ++k) { r.side[k] = side[k]; r.evj[k] = ev_join[k]; }
+    r.evf = ev_fork;
   }
   Run live(hipStream_t st) {
     Run r;
@@ -1725,6 +1840,7 @@ class EngineT : public Engine {
     r.dry = false;
     arena.dry = false;
     r.ar = &arena;
+    set_side(r);
     return r;
   }
 
@@ -1869,6 +1985,8 @@ class EngineT : public Engine {
       }
       Run r = live(priv);
       r.prof = &prof;
+      // per-launch event pairs time one stream: no side streams (nor in the dry pass above)
+      for (int k = 0; k < Run::kSide; ++k) r.side[k] = nullptr;
       prof.begin_pass();
       record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
     } else {
@@ -1932,7 +2050,8 @@ class EngineT : public Engine {
   std::unique_ptr<VitNet<T>> vit;
   Arena arena;
   hipStream_t priv;
-  hipEvent_t ev_in, ev_out;
+  hipStream_t side[Run::kSide];  // the other branches of the UNet's split section
+  hipEvent_t ev_in, ev_out, ev_fork, ev_join[Run::kSide];
   uint64_t noise_offset = 0;     // global index of image 0 (sharded runs)
   void* zero_page = nullptr;
 };

@@ -120,6 +120,11 @@ struct Run {
   Profiler* prof = nullptr;
   const void* zero = nullptr;    // 256 zero bytes on the device (conv padding source)
   double flops = 0;              // executed FLOPs (2*MAC) accumulated by the launches
+  // Side streams + fork / join events: the UNet's lowest levels run as concurrent branches of a
+  // part of the batch each (UNetNet::forward); null: everything on st.
+  static constexpr int kSide = 3;
+  hipStream_t side[kSide] = {};
+  hipEvent_t evf = nullptr, evj[kSide] = {};
   template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
 };
 

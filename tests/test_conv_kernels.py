@@ -125,3 +125,20 @@ def test_small_grid_ring_depth_bit_identical():
     print(out.stdout)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert "c3i st: OK" in out.stdout and "MISMATCH" not in out.stdout, out.stdout
+
+
+@pytest.mark.gpu
+def test_swapped_geglu_projection_bit_identical():
+    """The SpatialTransformer's GEGLU projection (attention.py GEGLU: proj -> x * gelu(gate)) on
+    swapped-operand tiles with the register epilogue (weights packed so each lane holds the x and
+    gate accumulators of the same 8 output channels; engine.cpp Packer::geglu) against the
+    LDS-epilogue tile on the same bf16 operands, at both UNet shapes (512 -> 2x2048 and
+    256 -> 2x1024 on 32x32 x 8 images) and all four swapped tile sizes: bit-identical outputs
+    (same ordered MFMA sums and epilogue arithmetic). Timing lines are printed."""
+    assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    out = subprocess.run([BIN, "gsw", "5"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert "gsw: OK" in out.stdout, out.stdout
+    rels = [float(v) for v in re.findall(r"rel (\S+)", out.stdout)]
+    assert len(rels) == 8 and all(v == 0.0 for v in rels), out.stdout
