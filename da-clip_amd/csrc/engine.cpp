@@ -760,7 +760,9 @@ struct UNetNet {
               const float* mw = nullptr; const float* mb = nullptr; int ss_off = 0; };
   struct LA { const float* gpre = nullptr; ConvW qkv; const float* wout = nullptr;
               const float* bout = nullptr; const float* gout = nullptr;
-              ConvW qkv_f; const float* qkv_cs = nullptr; };   // PreNorm folded into to_qkv (C = 256)
+              ConvW qkv_f; const float* qkv_cs = nullptr;     // PreNorm folded into to_qkv (C = 256)
+              const void* wqkv_g = nullptr;   // fused kernels: to_qkv diag(g) (the PreNorm gain)
+              float qshift = 0.f; };          // bound on |q| for la_apply's softmax (0: per-pixel max)
   struct ST { const float* gpre = nullptr; const float *gnw = nullptr, *gnb = nullptr;
               ConvW pin; const float *n1w = nullptr, *n1b = nullptr, *n3w = nullptr, *n3b = nullptr;
               ConvW qkv, o, ff1, ff2, pout; const float *a2v = nullptr, *a2o = nullptr, *a2ob = nullptr;
@@ -831,6 +833,25 @@ struct UNetNet {
         // folded into to_qkv like the SpatialTransformer's norm1.
         auto fq = P.fold_ln(a.la.qkv, pq, 384, C, p + "fn.norm.g", "", nullptr, {1, C, 1, 1});
         if (fq.cs) { a.la.qkv_f = fq.cw; a.la.qkv_cs = fq.cs; }
+      }
+      if (const HostW* g = P.ws.get(p + "fn.norm.g", {1, C, 1, 1}); g && pq.size() == (size_t)384 * C) {
+        // The fused kernels take the PreNorm gain inside to_qkv. |q_j| = |(Wq_j . g) . LN(x)| <=
+        // ||Wq_j . g|| sqrt(C) (||LN(x)|| <= sqrt(C)): with margin for the 16-bit operands, the
+        // largest over the 128 q rows is la_apply's softmax shift when <= 40 (e^-80 is normal).
+        std::vector<float> wg(pq.size());
+        double mx = 0;
+        for (int o = 0; o < 384; ++o) {
+          double n2 = 0;
+          for (int k = 0; k < C; ++k) {
+            wg[(size_t)o * C + k] = pq[(size_t)o * C + k] * g->v[k];
+            n2 += (double)wg[(size_t)o * C + k] * wg[(size_t)o * C + k];
+          }
+          if (o < 128) mx = std::max(mx, std::sqrt(n2));
+        }
+        a.la.wqkv_g = P.upload_T(wg, f + "to_qkv.weight", 1, C);
+        const double bound = 1.01 * mx * std::sqrt((double)C) + 0.05;
+        static const bool qs_on = !getenv("DAC_LA_QSHIFT") || atoi(getenv("DAC_LA_QSHIFT")) != 0;
+        a.la.qshift = (qs_on && bound <= 40.0) ? (float)bound : 0.f;
       }
       a.la.wout = P.f32(f + "to_out.0.weight", {C, 128, 1, 1});
       a.la.bout = P.f32(f + "to_out.0.bias", {C});
@@ -1138,7 +1159,7 @@ struct UNetNet {
     // C = 256 (the 64x64 level) takes the fused pair too on 16-bit handles (DAC_LA256=0: the
     // unfused chain below, for A/B).
     static const bool la256 = !getenv("DAC_LA256") || atoi(getenv("DAC_LA256")) != 0;
-    if (C == 64 || C == 128 || (C == 256 && sizeof(T) == 2 && la256)) {
+    if (la.wqkv_g && (C == 64 || C == 128 || (C == 256 && sizeof(T) == 2 && la256))) {
       // Fused (linattn.hip): context pass over x, then one apply pass x -> y (LN, q projection
       // and softmax, per-image to_out, its LayerNorm and the Residual).
       T* weff = r.alloc<T>((size_t)B * C * 128);
@@ -1146,7 +1167,7 @@ struct UNetNet {
       T* y = r.alloc<T>(M * C);
       r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32 + 2.0 * M * 128 * C;
       if (!r.dry)
-        linear_attention_fused<T>(x, la.gpre, la.qkv.w, la.wout, la.bout, la.gout, weff, y, B, H * W, C, ws, r.st);
+        linear_attention_fused<T>(x, la.wqkv_g, la.wout, la.bout, la.gout, weff, y, B, H * W, C, ws, r.st, la.qshift);
       emu_round<T>(r, y, C, M, C);
       return y;
     }

@@ -251,13 +251,14 @@ template <typename T>
 void linear_attention_weff(const void* qkv, const float* wout, void* weff, int B, int HW, int C,
                            float* ws, hipStream_t st, float hw_scale = 0.f);
 // Whole LinearAttention block, Residual(PreNorm(LinearAttention)) (module_util.py:27-33,
-// 89-97, 157-185), for C in {64, 128}: y = x + LN_out(to_out(ctx^T softmax_d(q))) with the
-// to_out bias and gain; weff: [B][C][128] scratch (per-image to_out weights), ws:
-// linear_attention_fused_ws_floats(B, HW) floats.
+// 89-97, 157-185), for C in {64, 128, 256}: y = x + LN_out(to_out(ctx^T softmax_d(q))) with the
+// to_out bias and gain; wqkv: to_qkv [384][C] with the PreNorm gain folded in (w diag(g));
+// weff: [B][C][128] scratch (per-image to_out weights), ws: linear_attention_fused_ws_floats(B, HW)
+// floats; qshift > 0: a bound on every |q| of the layer, used as the q-softmax shift (0: per-pixel max).
 template <typename T>
-void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, const float* wout,
-                            const float* bout, const float* gout, void* weff, void* y, int B, int HW,
-                            int C, float* ws, hipStream_t st);
+void linear_attention_fused(const void* x, const void* wqkv, const float* wout, const float* bout,
+                            const float* gout, void* weff, void* y, int B, int HW, int C, float* ws,
+                            hipStream_t st, float qshift = 0.f);
 size_t linear_attention_fused_ws_floats(int B, int HW);
 size_t linear_attention_ws_floats(int B, int HW);
 

@@ -337,8 +337,7 @@ template <> struct OpPack<float> {
 };
 
 template <typename T, int C>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 64 ? 2 : 1, 2))) la_proj_ctx(const T* __restrict__ x, const float* __restrict__ g,
-                                                   const T* __restrict__ w,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 64 ? 2 : 1, 2))) la_proj_ctx(const T* __restrict__ x, const T* __restrict__ w,
                                                    float* __restrict__ part, int HW, int nc, int CH,
                                                    float eps, float tau) {
   using K = LaCfg<T, C>;
@@ -383,7 +382,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
       xr[j] = (lp < TP && p < p1) ? *reinterpret_cast<const u32x4*>(xb + (size_t)p * C + (qq * K::QV + j) * VE)
                                   : u32x4{0u, 0u, 0u, 0u};
   };
-  // LayerNorm of the loaded pixel (two-pass in registers, like ln_kernel) -> LDS tile.
+  // LayerNorm of the loaded pixel (two-pass in registers, like ln_kernel) -> LDS tile. The
+  // PreNorm gain is folded into w (engine.cpp load_attn: w = to_qkv diag(g)).
   auto xstore = [&](int buf) {
     if (lp >= TP) return;
     float v[K::QV][VE];
@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
     for (int j = 0; j < K::QV; ++j) {
       float o[VE];
 #pragma unroll
-      for (int i = 0; i < VE; ++i) o[i] = (v[j][i] - mean) * rstd * g[(qq * K::QV + j) * VE + i];
+      for (int i = 0; i < VE; ++i) o[i] = (v[j][i] - mean) * rstd;
       store_vec<T>(reinterpret_cast<T*>(dst + K::swz(lp, qq * K::QV + j)), o);
     }
   };
@@ -474,11 +474,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
 #pragma unroll
       for (int jt = 0; jt < 2; ++jt) {
         float m = -INFINITY;
+        if constexpr (FULL && PT % 2 == 0) {
 #pragma unroll
-        for (int pt = 0; pt < PT; ++pt)
+          for (int pt = 0; pt < PT; pt += 2)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (FULL || t0 + pt * 16 + lg * 4 + r < p1) m = fmaxf(m, acc[pt][jt][r]);
+            for (int r = 0; r < 4; ++r) m = max3_raw(m, acc[pt][jt][r], acc[pt + 1][jt][r]);
+        } else {
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (FULL || t0 + pt * 16 + lg * 4 + r < p1) m = fmaxf(m, acc[pt][jt][r]);
+        }
         if (sizeof(T) == 4 || __any(m > mrun[jt] + tau)) {
           m = red16_max(m);
           m = red32_max(m);
@@ -712,10 +719,10 @@ template <typename T> DEV int la_perm(int p) {
 // tiles (the last one partial when HW % 16 != 0, e.g. the Wild-IR half-resolution levels),
 // nb sized so the whole grid is resident at once (no half-empty second round).
 template <typename T, int C>
-__global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const float* __restrict__ g,
-                                                const T* __restrict__ w, const T* __restrict__ weff,
+__global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const T* __restrict__ w,
+                                                const T* __restrict__ weff,
                                                 const float* __restrict__ bout, const float* __restrict__ gout,
-                                                T* __restrict__ y, int HW, float eps, float wscale) {
+                                                T* __restrict__ y, int HW, float eps, float wscale, float qshift) {
   constexpr int ES = sizeof(T), VE = TypeInfo<T>::VE, KSTEP = Mma<T>::KSTEP;
   constexpr int KS = C / KSTEP;                           // q-projection k-steps
   constexpr int KO = 128 / KSTEP;                         // out-GEMM k-steps
@@ -726,7 +733,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
   constexpr int QRB = C * ES, ERB = 128 * ES;
   constexpr int WROW = (QRB == 128 || QRB == 256) ? QRB : QRB + 16;
   constexpr int EROW = (ERB == 128 || ERB == 256) ? ERB : ERB + 16;
-  constexpr int SMEM = 128 * WROW + C * EROW;
+  constexpr int SMEM = 128 * WROW + C * EROW + 2 * C * 4;
   auto qoff = [](int row, int slot) {
     if constexpr (QRB == 128) return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4);
     else if constexpr (QRB == 256) return row * 256 + ((slot ^ (row & 15)) << 4);
@@ -740,6 +747,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char* sq = smem;                                        // Wq [128][C]
   char* sw = smem + 128 * WROW;                           // W_eff [C][128] permuted
+  float* sbo = reinterpret_cast<float*>(sw + C * EROW);   // to_out bias, then LayerNorm gain
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int b = blockIdx.y;
@@ -764,27 +772,22 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
       const int p = i / CPRE, k0 = (i % CPRE) * VE;
       *reinterpret_cast<u32x4*>(sw + eoff(p, k0 / VE)) = *reinterpret_cast<const u32x4*>(wb + (size_t)p * 128 + k0);
     }
+    for (int i = tid; i < 2 * C; i += 256) sbo[i] = i < C ? bout[i] : gout[i - C];
   }
-  // This lane's LayerNorm gains (channels ks*KSTEP + lg*VE + j) and epilogue terms.
-  float gx[KS][VE];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-    for (int j = 0; j < VE; ++j) gx[ks][j] = g[ks * KSTEP + lg * VE + j];
   __syncthreads();
 
   const int ntile = (p1 - p0 + 15) / 16;
-  u32x4 xr[KS];
-  auto xload = [&](int t) {
+  // Two x tiles in flight per wave (tiles t + 4 and t + 8 while t is processed): the loop body
+  // is written once (tile) and unrolled by 2 over the buffers xr0 / xr1.
+  u32x4 xr0[KS], xr1[KS];
+  auto xload = [&](u32x4 (&xr)[KS], int t) {
     const int px = p0 + t * 16 + lr;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       xr[ks] = px < p1 ? *reinterpret_cast<const u32x4*>(xb + (size_t)px * C + ks * KSTEP + lg * VE)
                        : u32x4{0u, 0u, 0u, 0u};
   };
-  int t = wv;
-  if (t < ntile) xload(t);
-  for (; t < ntile; t += 4) {
+  auto tile = [&](u32x4 (&xr)[KS], int t) {
     // The LDS weight fragments are loop-invariant; re-read them each tile instead of letting
     // the compiler hoist ~128 VGPRs of them out of the loop (occupancy).
     asm volatile("" ::: "memory");
@@ -813,11 +816,11 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
     for (int ks = 0; ks < KS; ++ks) {
       OpPack<T> pk;
 #pragma unroll
-      for (int j = 0; j < VE; ++j) pk.set(j, (v[ks][j] - mean) * rstd * gx[ks][j]);
+      for (int j = 0; j < VE; ++j) pk.set(j, (v[ks][j] - mean) * rstd);
       xf[ks] = pk.get();
     }
     const int tcur = t;
-    if (t + 4 < ntile) xload(t + 4);                      // next tile in flight
+    if (t + 8 < ntile) xload(xr, t + 8);                  // this buffer's next tile in flight
     // ---- q^T = Wq . xn^T : 8 tiles of 16 q channels.
     f32x4 aq[8];
 #pragma unroll
@@ -832,11 +835,17 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
     // ---- softmax over head hd = channels of tiles 2hd, 2hd+1 (rows 4lg + r on this lane).
 #pragma unroll
     for (int hd = 0; hd < 4; ++hd) {
-      float m = -INFINITY;
+      // Shift: qshift > 0 bounds every q of the layer (|q_j| <= ||Wq_j|| sqrt(C), set at load
+      // time only when <= 40, so exp(q - qshift) >= e^-80 stays a normal fp32 and the
+      // normalised softmax is unchanged); else the per-pixel head max.
+      float m = qshift;
+      if (!(qshift > 0.f)) {
+        m = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) m = fmaxf(m, fmaxf(aq[2 * hd][r], aq[2 * hd + 1][r]));
-      m = red16_max(m);
-      m = red32_max(m);
+        for (int r = 0; r < 4; ++r) m = max3_raw(m, aq[2 * hd][r], aq[2 * hd + 1][r]);
+        m = red16_max(m);
+        m = red32_max(m);
+      }
       float sm = 0.f;
       if constexpr (ES == 2) {
         // exp(a - m) = 2^(a log2e - m log2e): one v_fma + v_exp_f32 per element.
@@ -902,7 +911,7 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
         const int hf = ES == 2 ? ks >> 1 : ks >> 2;
         const int j = ES == 2 ? 2 * (ks & 1) + (jj >> 2) : ks & 3;
         const int r = ES == 2 ? jj & 3 : jj;
-        o[ks][jj] = fmaf(acc[hf][j][r], wscale, bout[ks * KSTEP + lg * VE + jj]);
+        o[ks][jj] = fmaf(acc[hf][j][r], wscale, sbo[ks * KSTEP + lg * VE + jj]);
         so += o[ks][jj];
       }
     so = red16_sum(so);
@@ -915,32 +924,39 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const f
       for (int jj = 0; jj < VE; ++jj) { const float d = o[ks][jj] - mo; qo += d * d; }
     qo = red16_sum(qo);
     qo = red32_sum(qo);
-    const float ro = 1.f / sqrtf(qo * (1.f / (float)C) + 1e-5f);
+    const float ro = rsq_t<T>(qo * (1.f / (float)C) + 1e-5f);
     if (px < p1) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         float oo[VE];
 #pragma unroll
         for (int jj = 0; jj < VE; ++jj)
-          oo[jj] = (o[ks][jj] - mo) * ro * gout[ks * KSTEP + lg * VE + jj] + v[ks][jj];
+          oo[jj] = (o[ks][jj] - mo) * ro * sbo[C + ks * KSTEP + lg * VE + jj] + v[ks][jj];
         store_vec<T>(yb + (size_t)px * C + ks * KSTEP + lg * VE, oo);
       }
     }
+  };
+  int t = wv;
+  if (t < ntile) xload(xr0, t);
+  if (t + 4 < ntile) xload(xr1, t + 4);
+  for (; t < ntile; t += 8) {
+    tile(xr0, t);
+    if (t + 4 < ntile) tile(xr1, t + 4);
   }
 }
 
 template <typename T>
-void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, const float* wout,
-                            const float* bout, const float* gout, void* weff, void* y, int B, int HW,
-                            int C, float* ws, hipStream_t st) {
+void linear_attention_fused(const void* x, const void* wqkv, const float* wout, const float* bout,
+                            const float* gout, void* weff, void* y, int B, int HW, int C, float* ws,
+                            hipStream_t st, float qshift) {
   const int nc = la_fused_chunks(HW, C), CH = la_chunk_px(HW, nc);
   float* part = ws;
   if (C == 64)
-    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
+    la_proj_ctx<T, 64><<<dim3(nc, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else if (C == 128)
-    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
+    la_proj_ctx<T, 128><<<dim3(nc, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else if constexpr (sizeof(T) == 2)
-    la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
+    la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else
     __builtin_trap();
   // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
@@ -967,21 +983,21 @@ void linear_attention_fused(const void* x, const float* gpre, const void* wqkv, 
   int nb = (per_cu * ncu + B - 1) / B;
   nb = std::max(1, std::min(nb, (HW + 63) / 64));
   if (C == 64)
-    la_apply<T, 64><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
-                                                 (T*)y, HW, 1e-5f, wscale);
+    la_apply<T, 64><<<dim3(nb, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                 (T*)y, HW, 1e-5f, wscale, qshift);
   else if (C == 128)
-    la_apply<T, 128><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
-                                                  (T*)y, HW, 1e-5f, wscale);
+    la_apply<T, 128><<<dim3(nb, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                  (T*)y, HW, 1e-5f, wscale, qshift);
   else if constexpr (sizeof(T) == 2)
-    la_apply<T, 256><<<dim3(nb, B), 256, 0, st>>>((const T*)x, gpre, (const T*)wqkv, (const T*)weff, bout, gout,
-                                                  (T*)y, HW, 1e-5f, wscale);
+    la_apply<T, 256><<<dim3(nb, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, (const T*)weff, bout, gout,
+                                                  (T*)y, HW, 1e-5f, wscale, qshift);
 }
 
-template void linear_attention_fused<float>(const void*, const float*, const void*, const float*, const float*,
-                                            const float*, void*, void*, int, int, int, float*, hipStream_t);
-template void linear_attention_fused<bf16>(const void*, const float*, const void*, const float*, const float*,
-                                           const float*, void*, void*, int, int, int, float*, hipStream_t);
-template void linear_attention_fused<f16>(const void*, const float*, const void*, const float*, const float*,
-                                          const float*, void*, void*, int, int, int, float*, hipStream_t);
+template void linear_attention_fused<float>(const void*, const void*, const float*, const float*, const float*,
+                                            void*, void*, int, int, int, float*, hipStream_t, float);
+template void linear_attention_fused<bf16>(const void*, const void*, const float*, const float*, const float*,
+                                            void*, void*, int, int, int, float*, hipStream_t, float);
+template void linear_attention_fused<f16>(const void*, const void*, const float*, const float*, const float*,
+                                            void*, void*, int, int, int, float*, hipStream_t, float);
 
 }  // namespace dac

@@ -19,6 +19,7 @@ extern "C" void dac_conv2_force(int v);
 extern "C" void dac_conv3r_enable(int on);
 extern "C" void dac_rbfuse_enable(int on);
 typedef __bf16 bf16;
+typedef _Float16 f16;
 
 struct Shape { const char* name; int B, H, W, cin, cout, kh, s, p, up, act, ss, res, kwp = 0, bias = 0; };
 
@@ -429,6 +430,55 @@ static int lnf_check(int iters) {
 // xn against a host LayerNorm (gain only, eps 1e-5) and the (mean, rstd) table against host
 // GroupNorm(32, eps 1e-6) moments of the host LayerNorm output; run twice (the per-image counters
 // must come back to zero).
+__global__ void fill_rand_h(f16* p, size_t n, uint32_t seed, float scale) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed * 0x9E3779B9u;
+  h ^= h >> 15; h *= 0x2c1b3c6dU; h ^= h >> 12; h *= 0x297a2d39U; h ^= h >> 15;
+  p[i] = (f16)(((h >> 8) / 16777216.f - 0.5f) * scale);
+}
+
+// LinearAttention block (linattn.hip, fp16) at the UNet's three LA shapes, B = 8: us per call
+// of the whole op (la_proj_ctx + la_combine_weff + la_apply; rocprofv3 splits the kernels) and a
+// checksum of the output (for comparing builds).
+static int la_bench(int iters, float qshift) {
+  struct Q { int HW, C; };
+  const Q shapes[] = {{256 * 256, 64}, {128 * 128, 128}, {64 * 64, 256}};
+  const int B = 8;
+  for (const Q& q : shapes) {
+    const int C = q.C, HW = q.HW;
+    const size_t n = (size_t)B * HW * C;
+    f16 *x, *y, *wqkv, *weff; float *gpre, *wout, *bout, *gout, *ws;
+    CK(hipMalloc(&x, n * 2)); CK(hipMalloc(&y, n * 2)); CK(hipMalloc(&wqkv, (size_t)3 * 128 * C * 2));
+    CK(hipMalloc(&weff, (size_t)B * C * 128 * 2));
+    CK(hipMalloc(&gpre, C * 4)); CK(hipMalloc(&wout, (size_t)C * 128 * 4)); CK(hipMalloc(&bout, C * 4)); CK(hipMalloc(&gout, C * 4));
+    CK(hipMalloc(&ws, linear_attention_fused_ws_floats(B, HW) * 4));
+    fill_rand_h<<<(n + 255) / 256, 256>>>(x, n, 5, 4.f);
+    fill_rand_h<<<(3 * 128 * C + 255) / 256, 256>>>(wqkv, 3 * 128 * C, 6, 0.5f);
+    fill_rand_f<<<1, 256>>>(gpre, C, 7, 1.f);
+    fill_rand_f<<<(C * 128 + 255) / 256, 256>>>(wout, C * 128, 8, 0.2f);
+    fill_rand_f<<<1, 256>>>(bout, C, 9, 0.2f);
+    fill_rand_f<<<1, 256>>>(gout, C, 10, 1.f);
+    auto run = [&]() { linear_attention_fused<f16>(x, wqkv, wout, bout, gout, weff, y, B, HW, C, ws, 0, qshift); };
+    run();
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) run();
+    CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<f16> h(n);
+    CK(hipMemcpy(h.data(), y, n * 2, hipMemcpyDeviceToHost));
+    double cs = 0, ca = 0;
+    for (size_t i = 0; i < n; ++i) { cs += (double)(float)h[i] * (double)((i % 977) + 1); ca += fabs((float)h[i]); }
+    printf("la %3dx%-3d C %3d  %7.1f us/op  checksum %.9e  abs %.9e\n", (int)sqrt((double)HW), (int)sqrt((double)HW), C,
+           ms * 1e3 / iters, cs, ca);
+    CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(wqkv)); CK(hipFree(weff)); CK(hipFree(gpre)); CK(hipFree(wout));
+    CK(hipFree(bout)); CK(hipFree(gout)); CK(hipFree(ws));
+  }
+  return 0;
+}
+
 static int gns_check() {
   int fails = 0;
   for (int C : {512, 256}) {
@@ -1194,6 +1244,7 @@ static int c3i_st_check(int iters) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "la")) return la_bench(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atof(argv[3]) : 0.f);
   if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
   if (argc > 1 && !strcmp(argv[1], "gsw")) return gsw_check(argc > 2 ? atoi(argv[2]) : 20);
 #ifdef DAC_STAMP
