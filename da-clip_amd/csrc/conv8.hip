@@ -1,9 +1,9 @@
 // conv8.hip — fp8 (OCP e4m3) implicit-GEMM convolution / linear layer on the block-scaled MFMA
-// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per clock), the MX weight path of
-// the fp8 handles (BASELINE configs[4]). Activations stay bf16 in HBM: every A tile is
+// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the 16-bit MFMA rate per clock), the MX weight path of
+// the fp8 handles (BASELINE configs[4]). Activations stay 16-bit (fp16, or bf16) in HBM: every A tile is
 // quantized on the fly while it is staged, with one E8M0 scale per (pixel, 64-channel block),
 // and the weights are quantized once at load with one E8M0 scale per (output channel,
-// 64-k block). Accumulation is fp32; the epilogue is the bf16 kernels' (conv_epi.h).
+// 64-k block). Accumulation is fp32; the epilogue is the 16-bit kernels' (conv_epi.h).
 //
 // Operand layout of the 16x16x128 scaled MFMA (measured on gfx950, tools/probes): lane
 // (r = l & 15, g = l >> 4) supplies 32 bytes of row r; the hardware treats them as k slots
@@ -22,7 +22,23 @@ namespace dac {
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
-template <int KH, int KW, int S, int P>
+// e4m3 pair conversion with an E8M0 scale, per 16-bit activation type.
+template <typename T> DEV short2_t cvt8(short2_t old, typename Vec8<T>::t2 v, float sc, bool hi);
+template <> DEV short2_t cvt8<bf16>(short2_t old, bf16x2_t v, float sc, bool hi) {
+  return hi ? __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(old, v, sc, true)
+            : __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(old, v, sc, false);
+}
+template <> DEV short2_t cvt8<f16>(short2_t old, f16x2_t v, float sc, bool hi) {
+  return hi ? __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(old, v, sc, true)
+            : __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(old, v, sc, false);
+}
+// |x| of the largest of a lane's packed 16-bit values (sign bits cleared, compared as integers:
+// both formats order non-negative values like their bit patterns) as a float.
+template <typename T> DEV float abs16_to_f(uint32_t m);
+template <> DEV float abs16_to_f<bf16>(uint32_t m) { return __builtin_bit_cast(float, m << 16); }
+template <> DEV float abs16_to_f<f16>(uint32_t m) { return (float)__builtin_bit_cast(f16, (uint16_t)m); }
+
+template <typename T, int KH, int KW, int S, int P>
 __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* __restrict__ w8,
                                                     const uint8_t* __restrict__ ws8, int Kp) {
   constexpr int BM = 128, BN = 128, WGM = 2, WGN = 2, TM = 4, TN = 4;
@@ -63,8 +79,8 @@ __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* _
       iw0 = ow * S - P;
     }
   }
-  const bf16* x1 = reinterpret_cast<const bf16*>(a.x1);
-  const bf16* x2 = reinterpret_cast<const bf16*>(a.x2);
+  const T* x1 = reinterpret_cast<const T*>(a.x1);
+  const T* x2 = reinterpret_cast<const T*>(a.x2);
   const int nrow = n0 + sr;
   const uint8_t* wrow = nrow < a.Cout ? w8 + (size_t)nrow * Kp : nullptr;
   const uint8_t* wsrow = nrow < a.Cout ? ws8 + (size_t)nrow * (Kp / 64) : nullptr;
@@ -79,7 +95,7 @@ __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* _
     const int kh = tap / KW, kw = tap - (tap / KW) * KW;
     const int ih = ih0 + kh, iw = iw0 + kw;
     ok = ok && (unsigned)ih < (unsigned)Hin && (unsigned)iw < (unsigned)Win;
-    const bf16* src = nullptr;
+    const T* src = nullptr;
     if (ok) {
       const int shh = a.up ? (ih >> 1) : ih, sww = a.up ? (iw >> 1) : iw;
       const size_t pix = (size_t)(pix0 + shh * a.Ws + sww);
@@ -102,7 +118,7 @@ __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* _
         const uint32_t v = ra[i][q] & 0x7fff7fffu;
         mx = max(mx, max(v & 0xffffu, v >> 16));
       }
-    const float p = __builtin_bit_cast(float, mx << 16);
+    const float p = abs16_to_f<T>(mx);
     int e = 0;
     if (p > 0.f) e = (int)ceilf(__log2f(p * (1.f / 448.f)));
     e = e < -126 ? -126 : (e > 126 ? 126 : e);
@@ -110,15 +126,15 @@ __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* _
     u32x4 q8[4];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      // 8 bf16 -> 8 fp8 (two dwords). The pairs are taken by shufflevector from the whole
-      // 8-vector: hipcc (ROCm 7.2) miscompiles __builtin_bit_cast(bf16x2_t, ra[i][q]) fed to
-      // this builtin (every call reads element 0 and the second result is dropped).
-      const bf16x8 w = __builtin_bit_cast(bf16x8, ra[i]);
+      // 8 16-bit values -> 8 fp8 (two dwords). The pairs are taken by shufflevector from the
+      // whole 8-vector: hipcc (ROCm 7.2) miscompiles __builtin_bit_cast(bf16x2_t, ra[i][q]) fed
+      // to this builtin (every call reads element 0 and the second result is dropped).
+      const typename Vec8<T>::t w = __builtin_bit_cast(typename Vec8<T>::t, ra[i]);
       short2_t lo = {0, 0}, hi = {0, 0};
-      lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_shufflevector(w, w, 0, 1), sc, false);
-      lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, __builtin_shufflevector(w, w, 2, 3), sc, true);
-      hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_shufflevector(w, w, 4, 5), sc, false);
-      hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, __builtin_shufflevector(w, w, 6, 7), sc, true);
+      lo = cvt8<T>(lo, __builtin_shufflevector(w, w, 0, 1), sc, false);
+      lo = cvt8<T>(lo, __builtin_shufflevector(w, w, 2, 3), sc, true);
+      hi = cvt8<T>(hi, __builtin_shufflevector(w, w, 4, 5), sc, false);
+      hi = cvt8<T>(hi, __builtin_shufflevector(w, w, 6, 7), sc, true);
       q8[i >> 1][(i & 1) * 2] = __builtin_bit_cast(uint32_t, lo);
       q8[i >> 1][(i & 1) * 2 + 1] = __builtin_bit_cast(uint32_t, hi);
     }
@@ -179,7 +195,7 @@ __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* _
   __syncthreads();                   // the epilogue's LDS tile overlays the last step's buffer
   const int mlast = (m0 + BM < M ? m0 + BM : M) - 1;
   const int bimg = (m0 / HWo == mlast / HWo) ? m0 / HWo : -1;
-  conv_epilogue_lds<bf16, BM, BN, WGM, WGN, EPR>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
+  conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR>(a, acc, smem, M, LinearRows{m0}, n0, HWo, bimg);
 }
 
 bool conv8_ok(const ConvArgs& a, int kh, int kw, int s, int p) {
@@ -189,13 +205,16 @@ bool conv8_ok(const ConvArgs& a, int kh, int kw, int s, int p) {
          a.w_bstride == 0 && !a.ln_g && !a.lnf_cs && !a.gna_stats && a.cwrap == 0 && a.Cout >= 32 && (kh > 1 || a.up == 0);
 }
 
+template <typename T>
 void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, const uint8_t* ws8, int Kp,
            hipStream_t st) {
   const int M = a.B * a.Ho * a.Wo;
   dim3 g((M + 127) / 128, (a.Cout + 127) / 128, 1);
-  if (kh == 3) conv8_kernel<3, 3, 1, 1><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
-  else if (kh == 1) conv8_kernel<1, 1, 1, 0><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
-  else conv8_kernel<4, 4, 2, 1><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
+  if (kh == 3) conv8_kernel<T, 3, 3, 1, 1><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
+  else if (kh == 1) conv8_kernel<T, 1, 1, 1, 0><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
+  else conv8_kernel<T, 4, 4, 2, 1><<<g, 256, 0, st>>>(a, w8, ws8, Kp);
 }
+template void conv8<bf16>(const ConvArgs&, int, int, int, int, const uint8_t*, const uint8_t*, int, hipStream_t);
+template void conv8<f16>(const ConvArgs&, int, int, int, int, const uint8_t*, const uint8_t*, int, hipStream_t);
 
 }  // namespace dac

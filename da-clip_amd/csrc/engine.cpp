@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace dac {
 
@@ -645,7 +646,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   if (a.xs8) {
     if constexpr (sizeof(T) == 2) conv3q<T>(a, cw.q8w, cw.q8s, r.st);
   } else if (use8) {
-    conv8(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
+    if constexpr (sizeof(T) == 2) conv8<T>(a, cw.kh, cw.kw, stride, pad, cw.w8, cw.ws8, cw.kp8, r.st);
   } else {
     conv<T>(a, cw.kh, cw.kw, stride, pad, r.st);
     // Diagnostic (DAC_DUP1X1=1): the 32x32-level 1x1 GEMMs run twice back to back (idempotent:
@@ -2080,7 +2081,14 @@ class EngineT : public Engine {
 std::unique_ptr<Engine> make_engine(int device, int dtype, const dac_config& cfg) {
   if (dtype == DAC_F32) return std::make_unique<EngineT<float>>(device, cfg);
   if (dtype == DAC_BF16) return std::make_unique<EngineT<bf16>>(device, cfg);
-  if (dtype == DAC_FP8) return std::make_unique<EngineT<bf16>>(device, cfg, true);
+  // fp8 handles: the e4m3 layers inside bf16 networks (measured 2.5 % faster than the same
+  // handles on an fp16 base, B = 16: 30.08 / 29.83 against 29.17 / 29.32 images/s);
+  // DAC_FP8_BASE=f16 runs every non-e4m3 layer in IEEE half instead.
+  if (dtype == DAC_FP8) {
+    static const bool h = getenv("DAC_FP8_BASE") && !strcmp(getenv("DAC_FP8_BASE"), "f16");
+    if (h) return std::make_unique<EngineT<f16>>(device, cfg, true);
+    return std::make_unique<EngineT<bf16>>(device, cfg, true);
+  }
   if (dtype == DAC_F16) return std::make_unique<EngineT<f16>>(device, cfg);
   throw Error(DAC_E_ARG, "dtype must be DAC_F32, DAC_BF16, DAC_FP8 or DAC_F16");
 }

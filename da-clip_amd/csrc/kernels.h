@@ -178,10 +178,11 @@ template <typename T>
 void conv_down(const ConvArgs& a, hipStream_t st);
 int conv_variant(const ConvArgs& a, int kh, int elem_bytes);
 
-// fp8 (e4m3, MX block scales) implicit GEMM for bf16 activations (conv8.hip): w8 [Cout][Kp]
+// fp8 (e4m3, MX block scales) implicit GEMM for bf16 / fp16 activations (conv8.hip): w8 [Cout][Kp]
 // e4m3 weights (K padded to Kp, a multiple of 128, with zeros), ws8 [Cout][Kp / 64] E8M0
 // exponents (weight = w8 * 2^(ws8 - 127)). conv8_ok: shapes / layouts it serves.
 bool conv8_ok(const ConvArgs& a, int kh, int kw, int s, int p);
+template <typename T>
 void conv8(const ConvArgs& a, int kh, int kw, int s, int p, const uint8_t* w8, const uint8_t* ws8, int Kp,
            hipStream_t st);
 // fp8 ResBlock pair (conv3q.hip). Producer: a 3x3 conv with ys8 set (block1, 16-bit input) whose

@@ -163,7 +163,7 @@ static int fp8_check() {
     a.x1 = dx; a.ld1 = sh.cin; a.C1 = sh.cin; a.Cin = sh.cin; a.Hs = sh.H; a.Ws = sh.W; a.B = sh.B;
     a.Ho = Ho; a.Wo = Wo; a.Cout = sh.cout; a.K = K; a.y = dy; a.ldy = sh.cout; a.zero = dz;
     if (!conv8_ok(a, sh.k, sh.k, sh.s, sh.p)) { printf("fp8 %-22s not eligible\n", sh.name); ++fails; continue; }
-    conv8(a, sh.k, sh.k, sh.s, sh.p, dw, ds, Kp, 0);
+    conv8<bf16>(a, sh.k, sh.k, sh.s, sh.p, dw, ds, Kp, 0);
     CK(hipDeviceSynchronize());
     std::vector<bf16> yb(yq.size());
     CK(hipMemcpy(yb.data(), dy, yb.size() * 2, hipMemcpyDeviceToHost));
