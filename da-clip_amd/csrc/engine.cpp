@@ -1404,7 +1404,7 @@ struct UNetNet {
     }
     // Section split (DAC_SPLIT_LVL: first level of the section, counted from the bottom, 0 = off;
     // DAC_SPLIT_N: branches).
-    static const int split_lvl = getenv("DAC_SPLIT_LVL") ? atoi(getenv("DAC_SPLIT_LVL")) : 1;
+    static const int split_lvl = getenv("DAC_SPLIT_LVL") ? atoi(getenv("DAC_SPLIT_LVL")) : 3;
     static const int split_n = getenv("DAC_SPLIT_N") ? atoi(getenv("DAC_SPLIT_N")) : 2;
     const int nbr = std::min({split_n, B, 1 + Run::kSide});
     const bool split = split_lvl > 0 && nbr >= 2 && r.side[nbr - 2];
@@ -1437,10 +1437,11 @@ struct UNetNet {
       cur = attn(r, mid_attn, cur, mid, B, h, w, cc);
       cur = resblock(r, mid2, cur, mid, nullptr, 0, B, h, w, ss);
     } else {
-      // The lowest split_lvl levels (the 32x32 level at 256^2 by default: downs[depth-1], the
-      // middle blocks, ups[0]) have small, latency-bound kernels, so with B >= 2
-      // they run as nbr concurrent branches of B / nbr images (streams r.st + r.side) whose
-      // prologues, epilogues and tails overlap. Every kernel is per-image (batch-invariant): the
+      // The lowest split_lvl levels (by default three: the 128x128, 64x64 and 32x32 levels at
+      // 256^2, i.e. downs[1..3], the middle blocks, ups[0..2]) have small, latency-bound kernels
+      // (DESIGN.md §9), so with B >= 2 they run as nbr concurrent branches of B / nbr images
+      // (streams r.st + r.side) whose prologues, epilogues and tails overlap. The 256^2 level
+      // stays one branch: its one-block-per-CU kernels (rbfuse, conv3w) would displace each other. Every kernel is per-image (batch-invariant): the
       // outputs are bit-identical to one full-batch branch. Output: the section's last sampling
       // conv, all images.
       const int C0 = levels[sl].first;
