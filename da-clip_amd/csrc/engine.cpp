@@ -1154,22 +1154,55 @@ struct UNetNet {
     return o;
   }
 
+  // Runs fn(run, first image, images) for nbr contiguous parts of the batch as concurrent
+  // branches: part 0 on r.st, part k on r.side[k - 1], forked from and joined back into r.st
+  // (recorded into the graph when r.st is capturing).
+  template <class F> void branches(Run& r, int B, int nbr, F&& fn) {
+    if (r.in_branch) throw Error(DAC_E_STATE, "nested branch fork");
+    if (!r.dry) {
+      HIP_OK(hipEventRecord(r.evf, r.st));
+      for (int k = 0; k + 1 < nbr; ++k) HIP_OK(hipStreamWaitEvent(r.side[k], r.evf, 0));
+    }
+    double fl = 0;
+    for (int k = 0; k < nbr; ++k) {
+      const int b0 = (int)((long)B * k / nbr), b1 = (int)((long)B * (k + 1) / nbr);
+      Run rk = r;
+      rk.st = k ? r.side[k - 1] : r.st;
+      rk.flops = 0;
+      rk.in_branch = true;
+      fn(rk, b0, b1 - b0);
+      fl += rk.flops;
+    }
+    r.flops += fl;
+    if (!r.dry)
+      for (int k = 0; k + 1 < nbr; ++k) {
+        HIP_OK(hipEventRecord(r.evj[k], r.side[k]));
+        HIP_OK(hipStreamWaitEvent(r.st, r.evj[k], 0));
+      }
+  }
+  bool la_fused(const LA& la, int C) const {
+    // C = 256 (the 64x64 level) takes the fused pair too on 16-bit handles (DAC_LA256=0: the
+    // unfused chain, for A/B).
+    static const bool la256 = !getenv("DAC_LA256") || atoi(getenv("DAC_LA256")) != 0;
+    return la.wqkv_g && (C == 64 || C == 128 || (C == 256 && sizeof(T) == 2 && la256));
+  }
+  // Fused (linattn.hip): context pass over x, then one apply pass x -> y (LN, q projection and
+  // softmax, per-image to_out, its LayerNorm and the Residual).
+  void linattn_fused(Run& r, const LA& la, const void* x, int C, int B, int H, int W, T* y) {
+    const size_t M = (size_t)B * H * W;
+    T* weff = r.alloc<T>((size_t)B * C * 128);
+    float* ws = r.alloc<float>(linear_attention_fused_ws_floats(B, H * W));
+    r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32 + 2.0 * M * 128 * C;
+    if (!r.dry)
+      linear_attention_fused<T>(x, la.wqkv_g, la.wout, la.bout, la.gout, weff, y, B, H * W, C, ws, r.st, la.qshift);
+    emu_round<T>(r, y, C, M, C);
+  }
   const void* linattn(Run& r, const LA& la, const void* x, int C, int B, int H, int W) {
     RoleScope rs(g_role == R_MID ? R_MID : R_LA);
     const size_t M = (size_t)B * H * W;
-    // C = 256 (the 64x64 level) takes the fused pair too on 16-bit handles (DAC_LA256=0: the
-    // unfused chain below, for A/B).
-    static const bool la256 = !getenv("DAC_LA256") || atoi(getenv("DAC_LA256")) != 0;
-    if (la.wqkv_g && (C == 64 || C == 128 || (C == 256 && sizeof(T) == 2 && la256))) {
-      // Fused (linattn.hip): context pass over x, then one apply pass x -> y (LN, q projection
-      // and softmax, per-image to_out, its LayerNorm and the Residual).
-      T* weff = r.alloc<T>((size_t)B * C * 128);
-      float* ws = r.alloc<float>(linear_attention_fused_ws_floats(B, H * W));
+    if (la_fused(la, C)) {
       T* y = r.alloc<T>(M * C);
-      r.flops += 2.0 * M * 384 * C + 2.0 * M * 4 * 32 * 32 + 2.0 * B * C * 128 * 32 + 2.0 * M * 128 * C;
-      if (!r.dry)
-        linear_attention_fused<T>(x, la.wqkv_g, la.wout, la.bout, la.gout, weff, y, B, H * W, C, ws, r.st, la.qshift);
-      emu_round<T>(r, y, C, M, C);
+      linattn_fused(r, la, x, C, B, H, W, y);
       return y;
     }
     T* qkv = r.alloc<T>(M * 384);
@@ -1441,36 +1474,20 @@ struct UNetNet {
       // 256^2, i.e. downs[1..3], the middle blocks, ups[0..2]) have small, latency-bound kernels
       // (DESIGN.md §9), so with B >= 2 they run as nbr concurrent branches of B / nbr images
       // (streams r.st + r.side) whose prologues, epilogues and tails overlap. The 256^2 level
-      // stays one branch: its one-block-per-CU kernels (rbfuse, conv3w) would displace each other. Every kernel is per-image (batch-invariant): the
-      // outputs are bit-identical to one full-batch branch. Output: the section's last sampling
-      // conv, all images.
+      // stays one branch: its one-block-per-CU kernels (rbfuse, conv3w) would displace each
+      // other. Every kernel is per-image (batch-invariant): the outputs are bit-identical to one
+      // full-batch branch. Output: the section's last sampling conv, all images.
       const int C0 = levels[sl].first;
       const int h0 = h, w0 = w;
       const size_t px = (size_t)h * w;
       if (sl != 0) { h *= 2; w *= 2; }
       const size_t pxo = (size_t)h * w;
       T* y = r.alloc<T>((size_t)B * pxo * C0);
-      if (!r.dry) {
-        HIP_OK(hipEventRecord(r.evf, r.st));
-        for (int k = 0; k + 1 < nbr; ++k) HIP_OK(hipStreamWaitEvent(r.side[k], r.evf, 0));
-      }
-      double fl = 0;
-      for (int k = 0; k < nbr; ++k) {
-        const int b0 = (int)((long)B * k / nbr), b1 = (int)((long)B * (k + 1) / nbr);
-        Run rk = r;
-        rk.st = k ? r.side[k - 1] : r.st;
-        rk.flops = 0;
-        section(rk, sl, static_cast<const T*>(cur) + b0 * px * C0, b1 - b0, h0, w0,
+      branches(r, B, nbr, [&](Run& rk, int b0, int nb) {
+        section(rk, sl, static_cast<const T*>(cur) + b0 * px * C0, nb, h0, w0,
                 ss ? ss + (size_t)b0 * ss_total : nullptr, cc ? cc + (size_t)b0 * cc_total : nullptr,
                 y + b0 * pxo * C0);
-        fl += rk.flops;
-      }
-      r.flops += fl;
-      if (!r.dry)
-        for (int k = 0; k + 1 < nbr; ++k) {
-          HIP_OK(hipEventRecord(r.evj[k], r.side[k]));
-          HIP_OK(hipStreamWaitEvent(r.st, r.evj[k], 0));
-        }
+      });
       cur = y;
     }
     for (int j = depth - sl; j < depth; ++j) {

@@ -125,6 +125,7 @@ struct Run {
   static constexpr int kSide = 3;
   hipStream_t side[kSide] = {};
   hipEvent_t evf = nullptr, evj[kSide] = {};
+  bool in_branch = false;        // recording one branch of a fork (no nested forks)
   template <class X> X* alloc(size_t n) { return reinterpret_cast<X*>(ar->get(n * sizeof(X))); }
 };
 
