@@ -2289,10 +2289,12 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         // Chosen from ONE image's tile count (64 = the batch-8 grid's 512): the two forms walk
         // the channels in different chunk orders (CK), so a batch-size-driven choice made an
         // image's result depend on its batch (B = 16 vs 1 at the 32x32 level).
+        // The 8-wave form as 4 x 2 waves of 32 x 64 (round 5: +0.3 % in the network against
+        // 2 x 4 waves of 64 x 32, three interleaved pairs; 4 x 4 waves of 32 x 32 no better).
         if ((long)(a.Ho * a.Wo / 128) * g.y >= 64)
           conv3_launch<T, 128, 128, 2, 2, 64>(a, g, conv3_rw(a, 128), st);
         else
-          conv3_launch<T, 128, 128, 2, 4, 128>(a, g, conv3_rw(a, 128), st);
+          conv3_launch<T, 128, 128, 4, 2, 128>(a, g, conv3_rw(a, 128), st);
         return;
       }
     }
