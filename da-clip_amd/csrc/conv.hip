@@ -8,10 +8,12 @@ namespace dac {
 
 int g_conv3_force = -1;
 int g_conv2_force = 0;
-// Tuning aid: DAC_CONV2_FORCE32=k forces 1x1 configuration k on the small-image GEMMs only
-// (Ho*Wo <= 1024: the SpatialTransformer level; GEGLU projections keep their tile), for in-network
-// sweeps.
-int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 0;
+// DAC_CONV2_FORCE32=k: 1x1 configuration k for the small-image plain GEMMs (256 <= Ho*Wo <= 1024:
+// the SpatialTransformer level; GEGLU projections and the LN / GroupNorm folds keep their tiles).
+// Default 18, swapped 128x128 tiles with a 4-stage ring: with the lowest levels split into two
+// half-batch branches it measured +0.6-0.8 % over the 64x128 tiles (four interleaved pairs,
+// DESIGN.md §9); 0 = the general dispatch.
+int g_conv2_force32 = getenv("DAC_CONV2_FORCE32") ? atoi(getenv("DAC_CONV2_FORCE32")) : 18;
 int g_conv3_buf = getenv("DAC_CONV3_BUF") ? atoi(getenv("DAC_CONV3_BUF")) : 1;
 int g_conv3h_on = getenv("DAC_CONV3H") ? atoi(getenv("DAC_CONV3H")) : 0;
 int g_c3i_st = getenv("DAC_C3I_ST") ? atoi(getenv("DAC_C3I_ST")) : 3;
