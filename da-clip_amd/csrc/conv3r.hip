@@ -106,6 +106,7 @@ bool conv3r_ok(const ConvArgs& a) {
 // the 256-VGPR limit of 2 waves per SIMD).
 template <typename T, int CIN, bool RES, bool SILU, bool FUSE>
 __global__ void __launch_bounds__(256, 2) conv3r_kernel(ConvArgs a, int RB) {
+  kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
   using G = C3R<CIN>;
   constexpr int JT = G::JT, NC = G::NC, SW = G::SW, NI = G::NI;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];

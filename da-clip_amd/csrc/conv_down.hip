@@ -38,6 +38,7 @@ bool conv_down_ok(const ConvArgs& a) {
 template <typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_down_kernel(ConvArgs a) {
+  kernarg_touch<sizeof(ConvArgs)>();                     // every kernarg line once, one wait (common.h)
   __shared__ __attribute__((aligned(1024))) char smem[2 * CD_STAGE];
   using SB = RowSwz<4, 1>;                         // 64-byte rows read 16 consecutive at a time
   const int tid = threadIdx.x, lane = tid & 63;

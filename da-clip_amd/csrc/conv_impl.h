@@ -863,6 +863,7 @@ inline int conv3_rw(const ConvArgs& a, int BM = 256) {
 // arithmetic per DMA instruction (v3 spent ~3 VALU per MFMA there). One row pitch required.
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, bool BUF = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
+  kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
@@ -1098,6 +1099,7 @@ template <int SLOTS, int TM> struct RowSwz {
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL = 0, int EPK = EPI_MIN, int WPE = 2>
 __global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 conv3i_kernel(ConvArgs a, int RW) {
+  kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
@@ -1661,6 +1663,7 @@ struct C3W {
 // (the flat form spent ~55 VALU per stage there). Needs one row pitch (ld2 == ld1 when split).
 template <typename T, int NWV, int TM = 4, int NST = 2, bool BUF = false, bool Q8 = false>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
+  kernarg_touch<sizeof(ConvArgs) + 8>();                     // every kernarg line once, one wait (common.h)
   using CF = C3W<NWV, TM, NST>;
   constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
   using SA = RowSwz<4, TM>;

@@ -116,6 +116,7 @@ bool rbfuse_ok(const RbArgs& a) {
 
 template <typename T, int CIN>
 __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
+  kernarg_touch<sizeof(RbArgs) + 4>();                     // every kernarg line once, one wait (common.h)
   using G = RBF<CIN>;
   constexpr int JT = G::JT, SW = G::SW, NC1 = G::NC1, EV = 4 * JT;
   constexpr bool FUSE = CIN == 128;
