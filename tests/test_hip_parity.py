@@ -376,3 +376,48 @@ def test_plain_encode_image_matches_reference(golden, dt):
     assert rel(m.encode_image(img, normalize=True).cpu().numpy(), g["b32_norm"]) < tol
     ic, dc = m.encode_image(img, control=True)          # the control path is unaffected
     assert rel(ic.cpu().numpy(), golden("daclip_b32_encode.npz")["image_context"]) < tol
+
+
+_SPLIT_SCRIPT = r"""
+import os, sys
+import numpy as np
+import torch
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "da-clip_amd")]
+from daclip_amd import arch, synth
+from daclip_amd.unet import ConditionalUNet
+sd = synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), seed=0)
+m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype="fp16")
+m.load_state_dict(sd)
+T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+x = T(synth.synth_noise((4, 3, 64, 64), seed=41, tag="sp") * 0.3 + 0.5)
+mu = T(synth.synth_images(4, 64, 64, seed=42))
+tc = T(synth.synth_noise((4, 512), seed=43, tag="tc"))
+ic = T(synth.synth_noise((4, 512), seed=44, tag="ic"))
+np.save(sys.argv[2], m(x, mu, 37.0, text_context=tc, image_context=ic).cpu().numpy())
+"""
+
+
+def test_unet_split_branches_bit_identical(tmp_path):
+    """The lowest levels recorded as two concurrent half-batch branches (engine.cpp
+    UNetNet::section, the default DAC_SPLIT_LVL=3) against one branch (DAC_SPLIT_LVL=0), and four
+    branches of one image: bit-identical fp16 UNet outputs at B = 4, 64x64 (every kernel of the
+    section is per-image). Separate processes: the switch is read once per process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "split.py"
+    script.write_text(_SPLIT_SCRIPT)
+    outs = {}
+    for tag, env in (("off", {"DAC_SPLIT_LVL": "0"}), ("two", {}), ("four", {"DAC_SPLIT_N": "4"})):
+        e = dict(os.environ)
+        e.pop("DAC_SPLIT_LVL", None)
+        e.pop("DAC_SPLIT_N", None)
+        e.update(env)
+        path = tmp_path / f"{tag}.npy"
+        r = subprocess.run([sys.executable, str(script), root, str(path)], env=e, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs[tag] = np.load(path)
+    assert np.isfinite(outs["off"]).all()
+    assert np.array_equal(outs["off"], outs["two"]) and np.array_equal(outs["off"], outs["four"])
