@@ -7,10 +7,15 @@ and resident in HBM before the timed region. Weights are created on rank 0 and b
 over RCCL. Usage (driver contract):
     python bench.py --gpus N --steps K --warmup W
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Run the first way with N > 1 (no WORLD_SIZE in the environment), bench.py starts the N ranks
+itself: one `torch.distributed.run` child on 127.0.0.1, launched before any GPU call, whose
+exit code it returns. Under a launcher, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,56 +29,8 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "restored images/sec @256x256, 100 IR-SDE steps; PSNR vs ref; 1/2/4/8 MI355X"
 MFMA_PEAK = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3, "fp8": 5000.0}   # dense TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0                                  # GB/s
-# Kernel symbol of each timed conv class (kh*100 + conv_variant) per dtype, to look up its
-# PMC traffic in profiles/pmc_traffic.json (tools/pmc_bench.sh + tools/pmc_traffic.py).
-KERNEL_SYMBOL = {
-    # class 312 = v4 256x64 swapped-operand tiles, plain (FL 12) and with the fused res_conv
-    # output (FL 28); FL bit 10 (1036 / 1052) = the buffer-resource DMA form the dispatcher takes
-    # whenever the input has one row pitch.
-    # (rocprofv3 prints fp32 instantiations demangled, the _Float16 / bfloat16 ones mangled)
-    (312, "fp32"): ("void dac::conv3i_kernel<float, 256, 64, 4, 1, 64, 2, 4, 0, 2>(dac::ConvArgs, int)",
-                    "_ZN3dac13conv3i_kernelIfLi256ELi64ELi4ELi1ELi64ELi2ELi4ELi0ELi2EEEvNS_8ConvArgsEi"),
-    (306, "fp32"): ("void dac::conv3_kernel<float, 128, 64, 2, 2, 64>(dac::ConvArgs, int)",
-                    "_ZN3dac12conv3_kernelIfLi128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"),
-    (307, "fp32"): ("void dac::conv3_kernel<float, 128, 128, 2, 2, 64>(dac::ConvArgs, int)",
-                    "_ZN3dac12conv3_kernelIfLi128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"),
-}
-for _dt, _m in (("bf16", "DF16b"), ("fp16", "DF16_")):
-    KERNEL_SYMBOL[(312, _dt)] = tuple(
-        f"_ZN3dac13conv3i_kernelI{_m}Li256ELi64ELi4ELi1ELi64ELi2ELi{fl}ELi0ELi2EEEvNS_8ConvArgsEi"
-        for fl in (12, 28, 1036, 1052))
-    KERNEL_SYMBOL[(321, _dt)] = f"_ZN3dac13conv3w_kernelI{_m}Li8ELi4ELi2EEEvNS_8ConvArgsEii"
-    KERNEL_SYMBOL[(306, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi64ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
-    KERNEL_SYMBOL[(307, _dt)] = f"_ZN3dac12conv3_kernelI{_m}Li128ELi128ELi2ELi2ELi64EEEvNS_8ConvArgsEi"
-    # class 327 = conv3r (conv3r.hip: register-stationary 3x3, CIN 64 / 128, epilogue variants)
-    KERNEL_SYMBOL[(327, _dt)] = tuple(
-        f"_ZN3dac13conv3r_kernelI{_m}Li{cin}ELb{res}ELb{silu}ELb{fuse}EEEvNS_8ConvArgsEi"
-        for cin in (64, 128) for res in (0, 1) for silu in (0, 1) for fuse in (0, 1))
-    # class 350 = the fused ResBlock (rbfuse.hip: block1 + block2 (+ res_conv) in one launch)
-    KERNEL_SYMBOL[(350, _dt)] = tuple(f"_ZN3dac13rbfuse_kernelI{_m}Li{cin}EEEvNS_6RbArgsEi" for cin in (64, 128))
-# fp8 handles: class 340 = conv3q (e4m3 64 -> 64 ResBlock block2 on the block-scaled MFMA).
-KERNEL_SYMBOL[(340, "fp8")] = "_ZN3dac13conv3q_kernelIDF16bEEvNS_8ConvArgsEPKhS3_ii"
+# Per-dispatch PMC figures by kernel symbol (tools/pmc_bench.sh + tools/pmc_traffic.py).
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-
-
-def pmc_entry(kernel_id, dtype):
-    """Per-dispatch PMC figures of the timed kernel class (same bench workload), or None. A
-    class served by several kernel symbols is averaged over their dispatches."""
-    syms = KERNEL_SYMBOL.get((kernel_id, dtype))
-    if syms is None or not os.path.exists(PMC_FILE):
-        return None
-    if isinstance(syms, str):
-        syms = (syms,)
-    with open(PMC_FILE) as f:
-        ks = json.load(f)["kernels"]
-    es = [ks[s] for s in syms if s in ks and "hbm_bytes_per_dispatch" in ks[s]]
-    if not es:
-        return None
-    n = sum(e["dispatches"] for e in es)
-    out = {"dispatches": n, "hbm_bytes_per_dispatch": sum(e["hbm_bytes_total"] for e in es) / n}
-    if all("mfma_busy" in e for e in es):
-        out["mfma_busy"] = sum(e["mfma_busy"] * e["dispatches"] for e in es) / n
-    return out
 
 
 def parse():
@@ -105,14 +62,23 @@ def parse():
                         "fp16 (equal-batch comparison for fp8), fp32 = the parity mode on the main workload; "
                         "'none' to skip")
     p.add_argument("--kernel-id", type=int, default=None,
-                   help="conv class timed for the roofline (kh*100 + variant, e.g. 312 = 3x3 interleaved-row "
-                        "v4 tiles, 327 = conv3r, 340 = conv3q); default: the class with the largest total time "
-                        "in one eager restore")
+                   help="time one conv class by eager per-launch HIP events instead (kh*100 + variant, e.g. "
+                        "312 = 3x3 interleaved-row v4 tiles, 327 = conv3r); default: the kernel symbol with the "
+                        "largest in-graph time, from a stamped replay of the captured loop graph")
+    p.add_argument("--eager-events", action="store_true",
+                   help="also time the roofline kernel's class by HIP events around each launch of an eager "
+                        "replay (secondary figure: that replay has no side-stream branches)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-roofline", action="store_true", help="skip the eager profiled replay (PMC runs)")
+    p.add_argument("--no-roofline", action="store_true", help="skip the profiled replays (PMC runs)")
     p.add_argument("--no-psnr", action="store_true", help="skip the PSNR-vs-reference sample")
     p.add_argument("--cpu-steps", type=int, default=5, help="UNet steps in the CPU sample (>= 5)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher / rank wiring check without a GPU: gloo backend, CPU tensors, one "
+                        "shard_inputs -> all-gather -> max-over-ranks timing pass; rank 0 prints the JSON "
+                        "line with n_gpus and the ranks it saw (tests/test_bench_dist.py)")
     a = p.parse_args()
+    if a.gpus < 1:
+        p.error("--gpus must be >= 1")
     wild = a.model == "wild-ir"
     a.batch = a.batch or (2 if wild else 8)
     a.res = a.res or (512 if wild else 256)
@@ -129,18 +95,70 @@ def model_setup(args):
         arch.VIT_B_32, arch.TEXT_B_32
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) outside a launcher: one process per GPU, started as a
+    `torch.distributed.run` child (one node, rendezvous on 127.0.0.1) running this same
+    command line. The parent has made no GPU call and never execs; it waits and returns the
+    child's exit code (the reference's multi-device path is DataParallel,
+    config/daclip-sde/models/denoising_model.py:37-42; here it is process-per-GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
 def setup_dist(args):
+    """Rank wiring from the launcher's environment. WORLD_SIZE must equal --gpus; the world
+    size reported as n_gpus is the process group's own."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if ws != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}: launch with "
+                         f"--nproc-per-node {args.gpus}, or run `bench.py --gpus {args.gpus}` alone")
+    import datetime
+    # A hung rank fails the run after DAC_DIST_TIMEOUT seconds (default 600) instead of
+    # stalling it: the RCCL broadcast / all-gather / barriers all inherit this timeout.
+    tmo = datetime.timedelta(seconds=float(os.environ.get("DAC_DIST_TIMEOUT", "600")))
+    if args.dry_run:
+        if ws > 1:
+            dist.init_process_group("gloo", timeout=tmo)
+    else:
+        torch.cuda.set_device(local)
+        if ws > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     if ws > 1:
-        # A hung rank fails the run after DAC_DIST_TIMEOUT seconds (default 600) instead of
-        # stalling it: the RCCL broadcast / all-gather / barriers all inherit this timeout.
-        import datetime
-        tmo = datetime.timedelta(seconds=float(os.environ.get("DAC_DIST_TIMEOUT", "600")))
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
+        ws, rank = dist.get_world_size(), dist.get_rank()
     return ws, rank, local
+
+
+def dry_run(args, ws, rank):
+    """The rank wiring of a bench run without a GPU (gloo, CPU tensors): this rank's shard of
+    the global batch, one all-gather of it (the restored-output gather's collective), the
+    max-over-ranks timing. Rank 0 prints the JSON line with n_gpus and the ranks seen."""
+    from daclip_amd import shard
+    R = 8
+    n_glob, lo, lq, _ = shard_inputs(args.batch, R, ws, rank, "cpu")
+    tag = torch.full((lq.shape[0], 1), float(rank))
+
+    def step():
+        return shard.gather_outputs(tag, n_glob)
+    out, el = timed_steps(step, args.warmup, args.steps, ws, "cpu")
+    ranks = sorted(set(int(v) for v in out[:, 0].tolist()))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": ws, "ranks_seen": ranks, "global_batch": n_glob,
+                          "shard_first_index": lo, "steps": args.steps, "warmup": args.warmup,
+                          "elapsed_s_max_over_ranks": el}), flush=True)
+    if ws > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def host_cores():
@@ -358,9 +376,10 @@ def timed_steps(step, warmup, steps, ws, dev):
 
 def profile_class(h, step, kernel_id):
     """Eager replay of one more restore of the same batch on the same stream with HIP events
-    around every launch of conv class `kernel_id` (HIP cannot time events recorded inside graph
-    replays). Returns (launches, mean ms per launch, FLOPs per launch, algorithmic bytes per
-    launch, eager ms), launches = 0 if the class does not occur."""
+    around every launch of conv class `kernel_id` (999 = every conv launch). The eager replay
+    records the UNet without its side-stream branches (full-batch launches), so it is a
+    secondary figure; the roofline comes from graph_profile. Returns (launches, mean ms per
+    launch, FLOPs per launch, algorithmic bytes per launch, eager ms, per-launch rows)."""
     from daclip_amd import _lib
     mean_ms, fl, by = _lib.ctypes.c_double(), _lib.ctypes.c_double(), _lib.ctypes.c_double()
     h.check(_lib.lib().dac_profile_enable(h.h, kernel_id), "profile_enable")
@@ -370,50 +389,193 @@ def profile_class(h, step, kernel_id):
     torch.cuda.synchronize()
     eager_ms = (time.perf_counter() - tp) * 1e3
     n = _lib.lib().dac_profile_read(h.h, _lib.ctypes.byref(mean_ms), _lib.ctypes.byref(fl), _lib.ctypes.byref(by))
+    rows = _launch_rows(h, n)
     h.check(_lib.lib().dac_profile_enable(h.h, -1), "profile_disable")
-    return max(n, 0), mean_ms.value, fl.value, by.value, eager_ms
+    return max(n, 0), mean_ms.value, fl.value, by.value, eager_ms, rows
+
+
+def _launch_rows(h, n):
+    """(ms, flops, bytes, class, label, symbol) of each launch of the last profile."""
+    from daclip_amd import _lib
+    c = _lib.ctypes
+    rows = []
+    for i in range(max(n, 0)):
+        ms, fl, by, cls, t0, br = c.c_double(), c.c_double(), c.c_double(), c.c_int(), c.c_double(), c.c_int()
+        lab, sym = c.create_string_buffer(200), c.create_string_buffer(400)
+        h.check(_lib.lib().dac_profile_launch(h.h, i, c.byref(ms), c.byref(fl), c.byref(by), c.byref(cls),
+                                              c.byref(t0), c.byref(br), lab, 200, sym, 400), "profile_launch")
+        rows.append((ms.value, fl.value, by.value, cls.value, lab.value.decode(), sym.value.decode(),
+                     t0.value, br.value))
+    return rows
+
+
+def time_shares(rows):
+    """Per launch: its in-graph duration divided among the conv launches running at the same
+    time (the UNet's split section runs two half-batch branches concurrently): the integral
+    over the launch's [start, end] of 1 / (number of profiled launches active). Sums to the
+    busy time of the profiled kernels; non-conv kernels of the other branch are not counted."""
+    ev = []
+    for i, r in enumerate(rows):
+        ev.append((r[6], 1, i))
+        ev.append((r[6] + r[0], -1, i))
+    ev.sort()
+    share = [0.0] * len(rows)
+    active = set()
+    last = None
+    for t, d, i in ev:
+        if last is not None and active and t > last:
+            w = (t - last) / len(active)
+            for j in active:
+                share[j] += w
+        last = t
+        if d > 0:
+            active.add(i)
+        else:
+            active.discard(i)
+    return share
+
+
+def graph_profile(h, step):
+    """Every conv launch of one restore timed INSIDE a replay of the captured loop graph
+    (dac_profile_mode 1): the engine records and captures the loop exactly as the timed graph
+    (same kernels, grids, arena and side-stream branches), each launch carrying a wall-clock
+    [begin, end] stamp pair it writes itself (HIP events cannot be timed inside graph
+    replays), replays it once with HIP events around the replay on the loop's stream, and
+    names each launch's kernel symbol from the captured graph's nodes.
+    Returns (per-launch rows, graph replay ms by HIP events, host ms of the profiled step)."""
+    from daclip_amd import _lib
+    L = _lib.lib()
+    h.check(L.dac_profile_mode(h.h, 1), "profile_mode")
+    try:
+        h.check(L.dac_profile_enable(h.h, 999), "profile_enable")
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        step_ms = (time.perf_counter() - tp) * 1e3
+        n = h.check(L.dac_profile_read(h.h, None, None, None), "profile_read")
+        rows = _launch_rows(h, n)
+        gms = _lib.ctypes.c_double()
+        h.check(L.dac_profile_graph_ms(h.h, _lib.ctypes.byref(gms)), "profile_graph_ms")
+    finally:
+        L.dac_profile_enable(h.h, -1)
+        L.dac_profile_mode(h.h, 0)
+    return rows, gms.value, step_ms
+
+
+def pmc_symbol(sym):
+    """Per-dispatch PMC figures of one kernel symbol (profiles/pmc_traffic.json), or None."""
+    if not sym or not os.path.exists(PMC_FILE):
+        return None
+    with open(PMC_FILE) as f:
+        ks = json.load(f)["kernels"]
+    es = [ks[x] for x in sym.split("+") if x in ks and "hbm_bytes_per_dispatch" in ks[x]]
+    if not es:
+        return None
+    n = sum(e["dispatches"] for e in es)
+    out = {"dispatches": n, "hbm_bytes_per_dispatch": sum(e["hbm_bytes_total"] for e in es) / n}
+    if all("mfma_busy" in e for e in es):
+        out["mfma_busy"] = sum(e["mfma_busy"] * e["dispatches"] for e in es) / n
+    return out
+
+
+def _group(rows, key, shares=None):
+    g = {}
+    for i, (ms, fl, by, cls, lab, sym, t0, br) in enumerate(rows):
+        k = key(cls, sym)
+        e = g.setdefault(k, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "classes": set(),
+                             "symbols": set(), "branch": 0, "share_ms": 0.0})
+        e["launches"] += 1
+        e["ms"] += ms
+        e["flops"] += fl
+        e["bytes"] += by
+        e["classes"].add(cls)
+        e["symbols"].add(sym)
+        e["branch"] += br
+        e["share_ms"] += shares[i] if shares else ms
+    return g
+
+
+def dominant_roofline(h, step, dtype, step_ms, pmc_ok=False, eager=True):
+    """Roofline of the kernel (symbol) with the largest in-graph time per restore, from one
+    stamped replay of the captured loop graph (graph_profile): achieved = its launches'
+    algorithmic FLOPs / their summed in-graph durations. Also every symbol's and every conv
+    class's share, and (secondary) the eager per-launch HIP-event figure of the same class."""
+    rows, graph_ms, prof_step_ms = graph_profile(h, step)
+    if not rows:
+        return None
+    peak = MFMA_PEAK[dtype]
+    shares = time_shares(rows)
+    syms = _group(rows, lambda c, s: s or f"class {c}", shares)
+    dom, e = max(syms.items(), key=lambda kv: kv[1]["ms"])
+    ach = e["flops"] / (e["ms"] * 1e-3) / 1e12
+    pmc = pmc_symbol(dom) if pmc_ok else None
+    r = {"kernel": dom, "kernel_classes": sorted(e["classes"]),
+         "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+         "traffic": pmc["hbm_bytes_per_dispatch"] if pmc else None,
+         "traffic_source": ("profiles/pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (KiB->B, gfx950 x2 read "
+                            "correction) per dispatch of this symbol, rocprofv3 --pmc over this bench command")
+         if pmc else None,
+         "mfma_busy_pmc": round(pmc["mfma_busy"], 4) if pmc and "mfma_busy" in pmc else None,
+         "launches_per_restore": e["launches"], "mean_launch_us": round(e["ms"] / e["launches"] * 1e3, 2),
+         "flops_per_launch": e["flops"] / e["launches"], "algorithmic_bytes_per_launch": e["bytes"] / e["launches"],
+         "achieved_hbm_GBps": round(e["bytes"] / (e["ms"] * 1e-3) / 1e9, 1),
+         "ms_per_restore": round(e["ms"], 3),
+         "launches_in_concurrent_branches": e["branch"],
+         "frac_time_shared": round(e["flops"] / (e["share_ms"] * 1e-3) / 1e12 / peak, 4),
+         "frac_time_shared_note": ("FLOPs / the launches' in-graph time divided among the profiled (conv) "
+                                   "launches running at the same time (two half-batch branches share the chip "
+                                   "in the split section); frac uses the undivided durations"),
+         "measured_on": (f"in-graph launch durations: one replay of the captured {len(rows)}-conv-launch loop "
+                         f"graph (the timed graph's kernels, grids and side-stream branches) with a wall-clock "
+                         f"[begin, end] stamp pair per launch written by the kernel (s_memrealtime, 100 MHz); "
+                         f"replay {graph_ms:.1f} ms by HIP events on the loop's stream, profiled step "
+                         f"{prof_step_ms:.1f} ms vs timed step {step_ms:.1f} ms"),
+         "selection": "kernel symbol with the largest summed in-graph duration per restore"}
+    if pmc and "mfma_busy" in pmc:
+        r["mfma_busy_note"] = ("PMC MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) on "
+                               "dispatches serialised by counter collection (no branch overlap), at the "
+                               "profiled clock; frac = FLOPs / in-graph duration / 2.5 PF at the nominal clock")
+    r["symbols"] = [{"symbol": k, "classes": sorted(v["classes"]), "launches": v["launches"],
+                     "ms_per_restore": round(v["ms"], 3), "mean_us": round(v["ms"] / v["launches"] * 1e3, 2),
+                     "flops_per_launch": v["flops"] / v["launches"],
+                     "frac_of_peak": round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / peak, 4),
+                     "in_branches": v["branch"],
+                     "frac_time_shared": round(v["flops"] / (v["share_ms"] * 1e-3) / 1e12 / peak, 4)}
+                    for k, v in sorted(syms.items(), key=lambda kv: -kv[1]["ms"])[:16]]
+    cls = _group(rows, lambda c, s: c, shares)
+    r["classes"] = [{"class": k, "launches": v["launches"], "ms_per_restore": round(v["ms"], 3),
+                     "frac_of_peak": round(v["flops"] / (v["ms"] * 1e-3) / 1e12 / peak, 4)}
+                    for k, v in sorted(cls.items(), key=lambda kv: -kv[1]["ms"])]
+    r["conv_ms_per_restore_in_graph"] = round(sum(v["ms"] for v in cls.values()), 3)
+    r["conv_busy_ms_per_restore"] = round(sum(shares), 3)
+    r["conv_tflops_per_restore"] = round(sum(x[1] for x in rows) / 1e12, 3)
+    if eager:
+        # Secondary: the same class(es) by HIP events around each launch of an eager replay
+        # (no side-stream branches there: full-batch launches, so launch counts differ).
+        n, _, _, _, eager_ms, erows = profile_class(h, step, 999)
+        ecls = _group(erows, lambda c, s: c)
+        sel = [v for k, v in ecls.items() if k in e["classes"]]
+        if sel:
+            ms = sum(v["ms"] for v in sel)
+            fl = sum(v["flops"] for v in sel)
+            nl = sum(v["launches"] for v in sel)
+            r["eager_events"] = {"classes": sorted(e["classes"]), "launches": nl, "mean_launch_us": round(ms / nl * 1e3, 2),
+                                 "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4), "eager_step_ms": round(eager_ms, 1)}
+    return r
 
 
 def roofline_entry(kernel_id, dtype, n, mean_ms, fl, by, eager_ms, graph_ms, pmc=None):
+    """--kernel-id: one conv class by the eager per-launch HIP events (secondary method)."""
     ach = fl / (mean_ms * 1e-3) / 1e12
     return {"kernel": f"conv_kernel class {kernel_id} (kh*100 + variant, {dtype})",
             "bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_PEAK[dtype],
             "unit": "TFLOP/s", "frac": round(ach / MFMA_PEAK[dtype], 4),
             "traffic": pmc["hbm_bytes_per_dispatch"] if pmc else None,
-            "traffic_source": ("profiles/pmc_traffic.json: 2*FETCH_SIZE+WRITE_SIZE (KiB->B, gfx950 "
-                               "x2 read correction) per dispatch of this kernel, rocprofv3 --pmc over "
-                               "this bench command") if pmc else None,
-            "mfma_busy_pmc": round(pmc["mfma_busy"], 4) if pmc and "mfma_busy" in pmc else None,
             "launches_timed": n, "mean_launch_us": round(mean_ms * 1e3, 2),
             "flops_per_launch": fl, "algorithmic_bytes_per_launch": by,
-            "achieved_hbm_GBps": round(by / (mean_ms * 1e-3) / 1e9, 1),
             "measured_on": f"eager replay of one batch (events per launch), {eager_ms:.1f} ms vs graph "
                            f"{graph_ms:.1f} ms/step"}
-
-
-# Conv classes a line's dominant-kernel search times (kh*100 + conv_variant; engine.cpp conv_call).
-ROOF_CANDIDATES = (350, 327, 312, 321, 326, 307, 311, 306, 310, 320, 324, 322, 323, 340, 115, 116, 117, 118, 108)
-
-
-def dominant_roofline(h, step, dtype, graph_ms, pmc_ok=False):
-    """Roofline of the conv class with the largest total time in one eager restore (each class
-    timed by its own eager replay), plus every timed class's share (`classes`)."""
-    rows = []
-    for k in ROOF_CANDIDATES:
-        n, mean_ms, fl, by, eager_ms = profile_class(h, step, k)
-        if n > 0:
-            rows.append((n * mean_ms, k, n, mean_ms, fl, by, eager_ms))
-    if not rows:
-        return None
-    rows.sort(reverse=True)
-    _, k, n, mean_ms, fl, by, eager_ms = rows[0]
-    r = roofline_entry(k, dtype, n, mean_ms, fl, by, eager_ms, graph_ms, pmc_entry(k, dtype) if pmc_ok else None)
-    r["class_ms_per_restore"] = round(n * mean_ms, 3)
-    r["selection"] = "conv class with the largest eager total over " + ",".join(map(str, ROOF_CANDIDATES))
-    r["classes"] = [{"class": kk, "launches": nn, "ms_per_restore": round(nn * mm, 3),
-                     "frac_of_peak": round(ff / (mm * 1e-3) / 1e12 / MFMA_PEAK[dtype], 4)}
-                    for _, kk, nn, mm, ff, _, _ in rows]
-    return r
 
 
 LINES = {
@@ -465,14 +627,18 @@ def extra_line(args, name, dev):
         res["psnr"] = psnr_sample(a2, arch.unet_state_spec(ucfg), clip, unet, lq[:1], img[:1], dev)
     if model == "wild-ir" and not args.no_roofline:
         step = make_step(clip, sde, lq, img, lo, n, 1)
-        res["roofline"] = dominant_roofline(unet._h, step, a2.dtype, el / k * 1e3)
+        res["roofline"] = dominant_roofline(unet._h, step, a2.dtype, el / k * 1e3, eager=False)
     res["wall_s"] = round(time.perf_counter() - t0, 1)
     return res
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     ws, rank, local = setup_dist(args)
+    if args.dry_run:
+        return dry_run(args, ws, rank)
     dev = torch.device("cuda", local)
     from daclip_amd import arch, synth, _lib, shard
     from daclip_amd.unet import ConditionalUNet
@@ -514,12 +680,13 @@ def main():
     if not args.no_roofline:
         # Roofline of the dominant kernel class (HIP events per launch on the kernel's stream).
         if args.kernel_id is None:
-            roof = dominant_roofline(h, step, args.dtype, el / args.steps * 1e3, pmc_ok=default_wl)
+            roof = dominant_roofline(h, step, args.dtype, el / args.steps * 1e3, pmc_ok=default_wl,
+                                     eager=args.eager_events)
         else:
-            n_launch, mean_ms, fl, by, eager_ms = profile_class(h, step, args.kernel_id)
+            n_launch, mean_ms, fl, by, eager_ms, _ = profile_class(h, step, args.kernel_id)
             if n_launch > 0:
                 roof = roofline_entry(args.kernel_id, args.dtype, n_launch, mean_ms, fl, by, eager_ms,
-                                      el / args.steps * 1e3, pmc_entry(args.kernel_id, args.dtype) if default_wl else None)
+                                      el / args.steps * 1e3)
 
     psnr = None
     if rank == 0 and not args.no_psnr:

@@ -311,17 +311,23 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
     if (p.kernel_id < 0 || p.launches == 0) throw dac::Error(DAC_E_STATE, "nothing profiled");
     double tot = 0;
     std::map<std::string, std::array<double, 3>> by;   // label -> count, ms, flops
+    if (p.stamps && p.lms.size() != p.launches) throw dac::Error(DAC_E_STATE, "graph profile incomplete");
+    if (!p.stamps) p.lms.assign(p.launches, 0.0);
     for (size_t i = 0; i < p.launches; ++i) {
-      HIP_OK(hipEventSynchronize(p.ev[2 * i + 1]));
-      float ms = 0;
-      HIP_OK(hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]));
+      if (!p.stamps) {
+        HIP_OK(hipEventSynchronize(p.ev[2 * i + 1]));
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, p.ev[2 * i], p.ev[2 * i + 1]));
+        p.lms[i] = ms;
+      }
+      const double ms = p.lms[i];
       tot += ms;
-      if (i < p.labels.size()) {
+      if (p.kernel_id == dac::Profiler::ALL && i < p.labels.size()) {
         auto& v = by[p.labels[i]];
         v[0] += 1; v[1] += ms; v[2] += p.lflops[i];
       }
     }
-    if (!by.empty()) {                                  // per-shape report (kernel_id ALL)
+    if (!by.empty() && getenv("DAC_PROFILE_PRINT")) {   // per-shape report (kernel_id ALL)
       std::vector<std::pair<double, std::string>> rows;
       for (auto& kv : by) {
         char line[320];
@@ -341,6 +347,40 @@ int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
     return DAC_OK;
   });
   return rc < 0 ? rc : n;
+}
+
+int dac_profile_mode(dac_handle* h, int graph_stamps) {
+  return guard(h, [&]() -> int {
+    h->eng->prof.stamps = graph_stamps != 0;
+    return DAC_OK;
+  });
+}
+
+int dac_profile_launch(dac_handle* h, int i, double* ms, double* flops, double* bytes, int* kernel_class,
+                       double* start_ms, int* in_branch, char* label, int label_len, char* symbol,
+                       int symbol_len) {
+  return guard(h, [&]() -> int {
+    auto& p = h->eng->prof;
+    if (i < 0 || (size_t)i >= p.launches || (size_t)i >= p.lms.size())
+      throw dac::Error(DAC_E_ARG, "dac_profile_launch: index out of range (call dac_profile_read first)");
+    if (ms) *ms = p.lms[i];
+    if (flops) *flops = p.lflops[i];
+    if (bytes) *bytes = p.lbytes[i];
+    if (kernel_class) *kernel_class = p.lcls[i];
+    if (start_ms) *start_ms = (size_t)i < p.lt0.size() ? p.lt0[i] : -1.0;
+    if (in_branch) *in_branch = (size_t)i < p.lbranch.size() ? p.lbranch[i] : 0;
+    if (label && label_len > 0) snprintf(label, label_len, "%s", i < (int)p.labels.size() ? p.labels[i].c_str() : "");
+    if (symbol && symbol_len > 0) snprintf(symbol, symbol_len, "%s", i < (int)p.lsym.size() ? p.lsym[i].c_str() : "");
+    return DAC_OK;
+  });
+}
+
+int dac_profile_graph_ms(dac_handle* h, double* ms) {
+  return guard(h, [&]() -> int {
+    if (!ms) throw dac::Error(DAC_E_ARG, "null output");
+    *ms = h->eng->prof.graph_ms;
+    return DAC_OK;
+  });
 }
 
 const char* dac_last_error(dac_handle* h) { return h ? h->err.c_str() : "null handle"; }

@@ -7,6 +7,8 @@
 // VE = 16/sizeof(T) elements (8 bf16 / f16 or 4 f32).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <stdexcept>
 #include <stdint.h>
 
 typedef __bf16 bf16;
@@ -146,6 +148,26 @@ template <int BYTES> DEV void kernarg_touch() {
   for (int o = 0; o < BYTES; o += 64) acc ^= p[o / 4];
   asm volatile("s_waitcnt lgkmcnt(0)" ::"s"(acc) : "memory");
 }
+
+// In-graph launch timing (engine Profiler::stamps; HIP events cannot be timed inside graph
+// replays): a kernel declares `StampGuard sg(a.stamp);` first thing. With a non-null stamp
+// block (STAMP_SLOTS [begin, end] pairs of 64-bit words per launch) the first wave of every
+// block atomic-mins the wall clock into its slot's begin and, on every exit path, each wave
+// atomic-maxes the clock into the slot's end; the slot is blockIdx.x % STAMP_SLOTS, which spreads
+// the atomics over 64 addresses (one address for a whole grid serialised them and stretched the
+// profiled replay by a fifth). min(begin) .. max(end) over a launch's slots is its duration on the
+// constant-rate counter (s_memrealtime, 100 MHz; ticks to ms by hipDeviceAttributeWallClockRate).
+// Null (every production launch): one uniform branch.
+constexpr int STAMP_SLOTS = 64;
+struct StampGuard {
+  unsigned long long* s;
+  DEV explicit StampGuard(unsigned long long* p) : s(p ? p + 2 * (blockIdx.x % STAMP_SLOTS) : nullptr) {
+    if (s && threadIdx.x == 0) atomicMin(s, (unsigned long long)wall_clock64());
+  }
+  DEV ~StampGuard() {
+    if (s && (threadIdx.x & 63) == 0) atomicMax(s + 1, (unsigned long long)wall_clock64());
+  }
+};
 
 DEV float silu_f(float x) { return x / (1.f + expf(-x)); }
 DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

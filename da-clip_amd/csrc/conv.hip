@@ -248,7 +248,7 @@ template void conv_part_reduce<f16>(const ConvArgs&, hipStream_t);
 
 template <typename T>
 void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {
-  if (a.xs8) abort();                              // e4m3 inputs: conv3q only
+  if (a.xs8) throw std::invalid_argument("conv: e4m3 inputs are conv3q-only");
   if (kh == 3 && kw == 3 && s == 1 && p == 1) conv_dispatch<T, 3, 3, 1, 1>(a, st);
   else if (kh == 1 && kw == 1 && s == 1 && p == 0) conv_dispatch<T, 1, 1, 1, 0>(a, st);
   else if (kh == 4 && kw == 4 && s == 2 && p == 1) conv_dispatch<T, 4, 4, 2, 1>(a, st);

@@ -45,6 +45,7 @@ DEV void mma8(f32x4& acc, const i32x8& w, const i32x8& x, int sw, int sx) {
 template <typename T>
 __global__ void __launch_bounds__(64 * C3Q_WAVES)
 conv3q_kernel(ConvArgs a, const uint8_t* __restrict__ q8w, const uint8_t* __restrict__ q8s, int ntiles, int delay) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int NWV = C3Q_WAVES, TM = C3Q_TM, NF = TM + 2, SEG = C3Q_SEG, NI = C3Q_NI, STAGE = C3Q_STAGE;
   using SA = RowSwz<4, TM>;
   using SB = RowSwz<4, 1>;
@@ -238,7 +239,7 @@ bool conv3q_ok(const ConvArgs& a) {
 
 template <typename T>
 void conv3q(const ConvArgs& a, const uint8_t* q8w, const uint8_t* q8s, hipStream_t st) {
-  if (!conv3q_ok(a) || !q8w || !q8s) abort();
+  if (!conv3q_ok(a) || !q8w || !q8s) throw std::invalid_argument("conv3q: arguments rejected by conv3q_ok");
   const int ntiles = a.B * a.Ho * (a.Wo / C3Q_SEG);
   conv3q_kernel<T><<<conv3w_blocks(ntiles, C3Q_WAVES), 64 * C3Q_WAVES, 0, st>>>(a, q8w, q8s, ntiles, 6);
 }

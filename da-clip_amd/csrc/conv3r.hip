@@ -107,6 +107,7 @@ bool conv3r_ok(const ConvArgs& a) {
 template <typename T, int CIN, bool RES, bool SILU, bool FUSE>
 __global__ void __launch_bounds__(256, 2) conv3r_kernel(ConvArgs a, int RB) {
   kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   using G = C3R<CIN>;
   constexpr int JT = G::JT, NC = G::NC, SW = G::SW, NI = G::NI;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
@@ -358,7 +359,7 @@ static void conv3r_launch(const ConvArgs& a, hipStream_t st) {
 
 template <typename T>
 void conv3r(const ConvArgs& a, hipStream_t st) {
-  if (!conv3r_ok(a)) abort();
+  if (!conv3r_ok(a)) throw std::invalid_argument("conv3r: arguments rejected by conv3r_ok");
   if (a.Cin == 64) conv3r_launch<T, 64>(a, st);
   else conv3r_launch<T, 128>(a, st);
 }

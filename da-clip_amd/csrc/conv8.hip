@@ -41,6 +41,7 @@ template <> DEV float abs16_to_f<f16>(uint32_t m) { return (float)__builtin_bit_
 template <typename T, int KH, int KW, int S, int P>
 __global__ void __launch_bounds__(256) conv8_kernel(ConvArgs a, const uint8_t* __restrict__ w8,
                                                     const uint8_t* __restrict__ ws8, int Kp) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int BM = 128, BN = 128, WGM = 2, WGN = 2, TM = 4, TN = 4;
   constexpr int ROWB = 128;                                  // bytes per staged row (128 k fp8)
   constexpr int TILE = BM * ROWB;                            // 16 KB

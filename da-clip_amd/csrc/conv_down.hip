@@ -39,6 +39,7 @@ template <typename T>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_down_kernel(ConvArgs a) {
   kernarg_touch<sizeof(ConvArgs)>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   __shared__ __attribute__((aligned(1024))) char smem[2 * CD_STAGE];
   using SB = RowSwz<4, 1>;                         // 64-byte rows read 16 consecutive at a time
   const int tid = threadIdx.x, lane = tid & 63;

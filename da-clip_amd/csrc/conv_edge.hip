@@ -50,6 +50,7 @@ bool conv7_ok(const ConvArgs& a) {
 template <typename T, int NP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv7_kernel(ConvArgs a, int ntiles) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   __shared__ __attribute__((aligned(1024))) char smem[2 * C7_BUF];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -205,6 +206,7 @@ bool conv3n_ok(const ConvArgs& a) {
 
 template <typename T, int NP>
 __global__ void __launch_bounds__(256) conv3n_kernel(ConvArgs a, int ntiles) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   __shared__ __attribute__((aligned(1024))) char smem[CN_ST * CN_SLOT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lr = lane & 15, lg = lane >> 4;

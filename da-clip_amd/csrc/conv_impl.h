@@ -42,6 +42,7 @@ DEV TileId xcd_tile() {
 
 template <typename T, int BM, int BN, int WGM, int WGN, int KH, int KW, int S, int P>
 __global__ void __launch_bounds__(256) conv_kernel(ConvArgs a) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int BKE = 128 / sizeof(T);
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -390,6 +391,7 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 template <typename T, int BM, int BN, int WGM, int WGN, int STAGES, int KH, int KW, int S, int P,
           int EPK = EPI_ALL>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int BKE = 128 / sizeof(T);
@@ -864,6 +866,7 @@ inline int conv3_rw(const ConvArgs& a, int BM = 256) {
 template <typename T, int BM, int BN, int WGM, int WGN, int CK, bool BUF = false>
 __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int RW) {
   kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
@@ -1100,6 +1103,7 @@ template <typename T, int BM, int BN, int WGM, int WGN, int CK, int ST, int FL =
 __global__ void __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(WPE, WPE)))
 conv3i_kernel(ConvArgs a, int RW) {
   kernarg_touch<sizeof(ConvArgs) + 4>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int NW = WGM * WGN;
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
@@ -1664,6 +1668,7 @@ struct C3W {
 template <typename T, int NWV, int TM = 4, int NST = 2, bool BUF = false, bool Q8 = false>
 __global__ void __launch_bounds__(64 * NWV) conv3w_kernel(ConvArgs a, int ntiles, int delay) {
   kernarg_touch<sizeof(ConvArgs) + 8>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   using CF = C3W<NWV, TM, NST>;
   constexpr int NF = TM + 2, VE = 8, SEG = CF::SEG, NI = CF::NI, STAGE = CF::STAGE;
   using SA = RowSwz<4, TM>;
@@ -1876,6 +1881,7 @@ inline int conv3h_ntiles(const ConvArgs& a) { return a.B * (a.Ho / C3H_RH) * (a.
 // after the barrier (3-8 % faster; starting the blocks out of phase was 5-20 % slower).
 template <typename T, int FL = 1>
 __global__ void __launch_bounds__(512) conv3h_kernel(ConvArgs a, int ntiles) {
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   constexpr int TM = 4, NF = TM + 2, VE = 8, ES = 2;
   constexpr unsigned OOB = 0x80000000u;
   using SA = RowSwz<4, TM>;
@@ -2365,7 +2371,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
       }
       __builtin_trap();                          // conv_lnf_ok said a folding kernel takes it
     }
-    const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho * a.Wo <= 1024 && a.Ho * a.Wo >= 256 && a.ksplit <= 1 && a.act != ACT_GEGLU) ? g_conv2_force32 : g_conv2_force;
+    const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho > 1 && a.Wo > 1 && a.Ho * a.Wo <= 1024 && a.Ho * a.Wo >= 256 && a.ksplit <= 1 && a.act != ACT_GEGLU) ? g_conv2_force32 : g_conv2_force;
     if constexpr (KH == 1) if (f2 > 0) {
       switch (f2) {
         case 1: DAC_V2(256, 128, 4, 2, 3, 512)

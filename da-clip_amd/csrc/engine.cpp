@@ -539,6 +539,29 @@ struct Packer {
 // ============================================================================= launches
 Profiler::~Profiler() {
   for (auto e : ev) (void)hipEventDestroy(e);
+  if (sbuf) (void)hipFree(sbuf);
+}
+
+// Start of one timed launch: an event (eager replay) or the launch's stamp pair (graph mode).
+static unsigned long long* prof_begin(Profiler* p, hipStream_t st) {
+  if (p->stamps) {
+    if (p->used >= p->scap) throw Error(DAC_E_STATE, "profiler stamp slots not pre-allocated");
+    return p->sbuf + 2 * STAMP_SLOTS * p->used;
+  }
+  if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
+  HIP_OK(hipEventRecord(p->ev[2 * p->used], st));
+  return nullptr;
+}
+static void prof_end(Profiler* p, const Run& r, int cls, double fl, double by) {
+  if (!p->stamps) HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
+  p->lbranch.push_back(r.in_branch ? 1 : 0);
+  p->used++;
+  p->launches++;
+  p->flops += fl;
+  p->bytes += by;
+  p->lcls.push_back(cls);
+  p->lflops.push_back(fl);
+  p->lbytes.push_back(by);
 }
 
 // The kernel arguments of a conv_call (the fused res_conv's fields included when requested).
@@ -639,10 +662,7 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   if (a.xs8 && !(sizeof(T) == 2 && cw.q8w && conv3q_ok(a))) throw Error(DAC_E_STATE, "conv: fp8 input on a layer without fp8 weights / kernel");
   if (a.Cin % (16 / (int)sizeof(T)) || (a.x2 == nullptr && a.C1 < a.Cin))
     throw Error(DAC_E_ARG, "conv: bad channel layout");
-  if (timed) {
-    if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
-    HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
-  }
+  if (timed) a.stamp = prof_begin(p, r.st);
   if (a.xs8) {
     if constexpr (sizeof(T) == 2) conv3q<T>(a, cw.q8w, cw.q8s, r.st);
   } else if (use8) {
@@ -657,23 +677,17 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   emu_round<T>(r, y, ldy, (size_t)M, cw.cout);
   if (fused) emu_round<T>(r, e.y2, e.ldy2, (size_t)M, cw.cout);
   if (timed) {
-    HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
-    p->used++;
-    p->launches++;
-    p->flops += fl;
-    if (p->kernel_id == Profiler::ALL) {
-      char lab[160];
-      snprintf(lab, sizeof lab, "c%d %3dx%-3d%s s%d %4d->%-4d%s%s%s%s%s", cls, Hs, Ws, up ? "^" : " ",
-               stride, cw.cin_real, cw.cout, e.res1 ? " +r" : "", e.res2 ? " +r2" : "",
-               e.ss ? " ss" : "", e.w_bstride ? " perimg" : "", fused ? " +1x1" : "");
-      p->labels.push_back(lab);
-      p->lflops.push_back(fl);
-    }
+    char lab[160];
+    snprintf(lab, sizeof lab, "c%d %3dx%-3d%s B%d s%d %4d->%-4d%s%s%s%s%s", cls, Hs, Ws, up ? "^" : " ", B,
+             stride, cw.cin_real, cw.cout, e.res1 ? " +r" : "", e.res2 ? " +r2" : "",
+             e.ss ? " ss" : "", e.w_bstride ? " perimg" : "", fused ? " +1x1" : "");
+    p->labels.push_back(lab);
     // Algorithmic HBM bytes: every operand touched once (input, weights, output, residuals).
     // (e4m3 tensors: 1 byte per value + 2 exponent bytes per pixel; e4m3 weights 1 byte.)
     const double es = sizeof(T), ei = a.xs8 ? 1 + 2.0 / 64 : es, eo = a.ys8 ? 1 + 2.0 / 64 : es;
-    p->bytes += ei * B * Hs * Ws * cw.cin_real + (a.xs8 ? 1 : es) * cw.cout * cw.kh * cw.kw * cw.cin +
-                M * cw.cout * (eo + es * ((e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0)));
+    prof_end(p, r, cls, fl,
+             ei * B * Hs * Ws * cw.cin_real + (a.xs8 ? 1 : es) * cw.cout * cw.kh * cw.kw * cw.cin +
+                 M * cw.cout * (eo + es * ((e.res1 ? 1 : 0) + (e.res2 ? 1 : 0) + (fused ? 1 : 0))));
   }
 }
 
@@ -1081,24 +1095,14 @@ struct UNetNet {
           return o;
         }
         if (!rb.c1.w || !rb.c2.w || (rb.has_res && !rb.res.w)) throw Error(DAC_E_STATE, "conv weight not loaded");
-        if (timed) {
-          if (p->ev.size() < 2 * (p->used + 1)) throw Error(DAC_E_STATE, "profiler events not pre-created");
-          HIP_OK(hipEventRecord(p->ev[2 * p->used], r.st));
-        }
+        if (timed) ra.stamp = prof_begin(p, r.st);
         rbfuse<T>(ra, r.st);
         if (timed) {
-          HIP_OK(hipEventRecord(p->ev[2 * p->used + 1], r.st));
-          p->used++;
-          p->launches++;
-          p->flops += fl;
-          if (p->kernel_id == Profiler::ALL) {
-            char lab[160];
-            snprintf(lab, sizeof lab, "c350 %3dx%-3d  ResBlock %4d->%-4d fused", H, W, rb.c1.cin_real, rb.dout);
-            p->labels.push_back(lab);
-            p->lflops.push_back(fl);
-          }
+          char lab[160];
+          snprintf(lab, sizeof lab, "c350 %3dx%-3d  B%d ResBlock %4d->%-4d fused", H, W, B, rb.c1.cin_real, rb.dout);
+          p->labels.push_back(lab);
           // Algorithmic HBM bytes: x in, y out.
-          p->bytes += 2.0 * M * (rb.c1.cin_real + rb.dout);
+          prof_end(p, r, 350, fl, sizeof(T) * (double)M * (rb.c1.cin_real + rb.dout));
         }
         return o;
       }
@@ -1163,22 +1167,33 @@ struct UNetNet {
       HIP_OK(hipEventRecord(r.evf, r.st));
       for (int k = 0; k + 1 < nbr; ++k) HIP_OK(hipStreamWaitEvent(r.side[k], r.evf, 0));
     }
-    double fl = 0;
-    for (int k = 0; k < nbr; ++k) {
-      const int b0 = (int)((long)B * k / nbr), b1 = (int)((long)B * (k + 1) / nbr);
-      Run rk = r;
-      rk.st = k ? r.side[k - 1] : r.st;
-      rk.flops = 0;
-      rk.in_branch = true;
-      fn(rk, b0, b1 - b0);
-      fl += rk.flops;
-    }
-    r.flops += fl;
-    if (!r.dry)
+    // Every side stream is joined back into r.st on every exit, also when a branch throws
+    // (HIP error, arena overflow, missing weight): a capture left with a forked stream could
+    // not be ended, and the side streams would stay in capture mode for later calls.
+    auto join = [&]() {
+      if (r.dry) return;
       for (int k = 0; k + 1 < nbr; ++k) {
         HIP_OK(hipEventRecord(r.evj[k], r.side[k]));
         HIP_OK(hipStreamWaitEvent(r.st, r.evj[k], 0));
       }
+    };
+    double fl = 0;
+    try {
+      for (int k = 0; k < nbr; ++k) {
+        const int b0 = (int)((long)B * k / nbr), b1 = (int)((long)B * (k + 1) / nbr);
+        Run rk = r;
+        rk.st = k ? r.side[k - 1] : r.st;
+        rk.flops = 0;
+        rk.in_branch = true;
+        fn(rk, b0, b1 - b0);
+        fl += rk.flops;
+      }
+    } catch (...) {
+      try { join(); } catch (...) {}             // the branch's error is the one reported
+      throw;
+    }
+    r.flops += fl;
+    join();
   }
   bool la_fused(const LA& la, int C) const {
     // C = 256 (the 64x64 level) takes the fused pair too on 16-bit handles (DAC_LA256=0: the
@@ -2006,6 +2021,8 @@ class EngineT : public Engine {
     if (no_graph && prof.kernel_id < 0) {
       Run r = live(priv);
       record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
+    } else if (prof.kernel_id >= 0 && prof.stamps) {
+      profile_graph(b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
     } else if (prof.kernel_id >= 0) {
       // Profiling replay: HIP cannot report elapsed time between events recorded by graph
       // nodes (hipEventElapsedTime -> invalid handle), so the same launch sequence runs
@@ -2055,6 +2072,123 @@ class EngineT : public Engine {
     HIP_OK(hipMemcpyAsync(x, b.xs, n * 4, hipMemcpyDeviceToDevice, priv));
     HIP_OK(hipEventRecord(ev_out, priv));
     HIP_OK(hipStreamWaitEvent(st, ev_out, 0));
+  }
+
+  // Graph-mode profiling (Profiler::stamps): the loop is recorded and captured exactly as the
+  // timed graph (same arena, side-stream branches, kernels and grids), with a [begin, end]
+  // wall-clock stamp pair in every launch of the profiled class(es); one replay, bracketed by
+  // HIP events on the loop's stream, gives every launch's in-graph duration. The kernel symbol
+  // of each launch is read back from the captured graph's kernel nodes (the stamp pointer in
+  // their argument block names the launch).
+  void profile_graph(Bufs& b, int mode, int B, int H, int W, int nT, bool has_noise, bool has_tc,
+                     bool has_ic) {
+    Arena da;
+    Run d;
+    d.dry = true;
+    d.ar = &da;
+    d.prof = &prof;
+    d.zero = zero_page;
+    set_side(d);       // the same branch structure as the live capture
+    prof.begin_pass();
+    record_loop(d, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
+    const size_t n = prof.used;
+    if (n > prof.scap) {
+      if (prof.sbuf) HIP_OK(hipFree(prof.sbuf));
+      prof.sbuf = nullptr;
+      prof.scap = 0;
+      HIP_OK(hipMalloc(&prof.sbuf, 2 * STAMP_SLOTS * n * sizeof(unsigned long long)));
+      prof.scap = n;
+    }
+    stamp_init(prof.sbuf, (size_t)STAMP_SLOTS * n, priv);
+    Run r = live(priv);
+    r.prof = &prof;
+    prof.begin_pass();
+    hipGraph_t g = nullptr;
+    HIP_OK(hipStreamBeginCapture(priv, hipStreamCaptureModeThreadLocal));
+    try {
+      record_loop(r, b, mode, B, H, W, nT, has_noise, has_tc, has_ic);
+    } catch (...) {
+      hipGraph_t dead = nullptr;
+      (void)hipStreamEndCapture(priv, &dead);
+      if (dead) (void)hipGraphDestroy(dead);
+      throw;
+    }
+    HIP_OK(hipStreamEndCapture(priv, &g));
+    if (prof.used != n) {
+      (void)hipGraphDestroy(g);
+      throw Error(DAC_E_STATE, "profile_graph: dry and live recordings differ");
+    }
+    prof.lsym.assign(n, std::string());
+    size_t nn = 0;
+    if (hipGraphGetNodes(g, nullptr, &nn) == hipSuccess && nn) {
+      std::vector<hipGraphNode_t> nodes(nn);
+      if (hipGraphGetNodes(g, nodes.data(), &nn) == hipSuccess) {
+        for (size_t i = 0; i < nn; ++i) {
+          hipGraphNodeType ty;
+          if (hipGraphNodeGetType(nodes[i], &ty) != hipSuccess || ty != hipGraphNodeTypeKernel) continue;
+          hipKernelNodeParams kp{};
+          if (hipGraphKernelNodeGetParams(nodes[i], &kp) != hipSuccess || !kp.func || !kp.kernelParams ||
+              !kp.kernelParams[0])
+            continue;
+          const char* nm = hipKernelNameRefByPtr(kp.func, priv);
+          if (!nm) continue;
+          const std::string name(nm);
+          unsigned long long* sp = nullptr;
+          if (name.find("rbfuse_kernel") != std::string::npos)
+            sp = static_cast<const RbArgs*>(kp.kernelParams[0])->stamp;
+          else if (name.find("conv") != std::string::npos && name.find("_kernel") != std::string::npos)
+            sp = static_cast<const ConvArgs*>(kp.kernelParams[0])->stamp;
+          if (!sp || sp < prof.sbuf || sp >= prof.sbuf + 2 * STAMP_SLOTS * n) continue;
+          std::string& dst = prof.lsym[(size_t)(sp - prof.sbuf) / (2 * STAMP_SLOTS)];
+          dst = dst.empty() ? name : dst + "+" + name;
+        }
+      }
+    }
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_OK(ie);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    try {
+      HIP_OK(hipEventCreate(&e0));
+      HIP_OK(hipEventCreate(&e1));
+      HIP_OK(hipEventRecord(e0, priv));
+      HIP_OK(hipGraphLaunch(ex, priv));
+      HIP_OK(hipEventRecord(e1, priv));
+      HIP_OK(hipEventSynchronize(e1));
+      float ms = 0;
+      HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+      prof.graph_ms = ms;
+      std::vector<unsigned long long> hs(2 * STAMP_SLOTS * n);
+      HIP_OK(hipMemcpy(hs.data(), prof.sbuf, hs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      int khz = 0;
+      HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+      if (khz <= 0) throw Error(DAC_E_HIP, "profile_graph: no wall-clock rate");
+      prof.lms.assign(n, 0.0);
+      prof.lt0.assign(n, 0.0);
+      unsigned long long origin = ~0ull;
+      for (size_t i = 0; i < n; ++i) {
+        unsigned long long b0 = ~0ull, b1 = 0;
+        for (int k = 0; k < STAMP_SLOTS; ++k) {                // slots no block used stay [max, 0]
+          b0 = std::min(b0, hs[2 * (STAMP_SLOTS * i + k)]);
+          b1 = std::max(b1, hs[2 * (STAMP_SLOTS * i + k) + 1]);
+        }
+        if (b0 == ~0ull || b1 < b0)
+          throw Error(DAC_E_STATE, "profile_graph: launch " + std::to_string(i) + " left no stamps");
+        prof.lms[i] = (double)(b1 - b0) / (double)khz;        // ticks / kHz = ms
+        prof.lt0[i] = (double)b0;
+        origin = std::min(origin, b0);
+      }
+      for (size_t i = 0; i < n; ++i) prof.lt0[i] = (prof.lt0[i] - (double)origin) / (double)khz;
+    } catch (...) {
+      if (e0) (void)hipEventDestroy(e0);
+      if (e1) (void)hipEventDestroy(e1);
+      (void)hipGraphExecDestroy(ex);
+      throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIP_OK(hipGraphExecDestroy(ex));
   }
 
   void invalidate_graphs() override { clear_graphs(); }

@@ -109,7 +109,25 @@ struct Profiler {
   static constexpr int ALL = 999;
   std::vector<std::string> labels;
   std::vector<double> lflops;
-  void begin_pass() { used = 0; flops = 0; bytes = 0; launches = 0; labels.clear(); lflops.clear(); }
+  // Per timed launch: conv class, algorithmic bytes, and (graph mode) measured duration and
+  // kernel symbol.
+  std::vector<int> lcls;
+  std::vector<double> lbytes, lms;
+  std::vector<double> lt0;       // graph mode: launch start (ms after the replay's first launch)
+  std::vector<char> lbranch;     // launched inside a concurrent branch of the UNet's split section
+  std::vector<std::string> lsym;
+  // Graph mode (dac_profile_mode 1): the next dac_sde_reverse records its loop into a captured
+  // graph exactly as the timed loop does (side-stream branches included), every timed launch
+  // carrying a [begin, end] wall-clock stamp pair (ConvArgs::stamp) in sbuf; one replay of that
+  // graph gives every launch's in-graph duration. graph_ms = the replay's HIP-event time.
+  bool stamps = false;
+  unsigned long long* sbuf = nullptr;
+  size_t scap = 0;
+  double graph_ms = 0;
+  void begin_pass() {
+    used = 0; flops = 0; bytes = 0; launches = 0; labels.clear(); lflops.clear();
+    lcls.clear(); lbytes.clear(); lms.clear(); lsym.clear(); lt0.clear(); lbranch.clear(); graph_ms = 0;
+  }
   ~Profiler();
 };
 

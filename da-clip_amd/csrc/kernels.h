@@ -107,6 +107,10 @@ struct ConvArgs {
   // Null: only the 16-row-interleaved order in w / bias exists.
   const void* w_gs;
   const float* b_gs;
+  // In-graph launch timing (bench roofline, engine Profiler::stamps): null, or a [begin, end]
+  // pair of 64-bit device words: the kernel's first wave atomic-mins its start and every wave
+  // atomic-maxes its end on the constant-rate wall clock (common.h StampGuard).
+  unsigned long long* stamp;
 };
 // The dispatcher has an LN-folding kernel for this 1x1 GEMM (16-bit types only).
 bool conv_lnf_ok(const ConvArgs& a, int elem_bytes);
@@ -149,6 +153,7 @@ struct RbArgs {
   const void* wr;          // [64][Cin] (Cin = 128) or null
   const float* ss; int ss_ld;    // scale [b * ss_ld + n], shift [b * ss_ld + 64 + n]
   void* y; int ldy;
+  unsigned long long* stamp;     // in-graph launch timing, as ConvArgs::stamp
 };
 bool rbfuse_pays(const RbArgs& a);
 bool rbfuse_ok(const RbArgs& a);
@@ -280,6 +285,8 @@ void round_bf16_rows(float* y, int ld, size_t rows, int C, hipStream_t st);
 void ss_fill(float* ss, int C, float scale_m1, const float* shift, hipStream_t st);
 // p[0] = a, p[1] = b on the device, in stream order.
 void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st);
+// n [begin, end] stamp pairs reset to [UINT64_MAX, 0] (ConvArgs::stamp, engine Profiler).
+void stamp_init(unsigned long long* s, size_t n, hipStream_t st);
 // y[r, :] = softmax(x[r, :]) * v  (DenoisingUNet_arch.py:134)
 void softmax_mul(const float* x, const float* v, float* y, int R, int C, hipStream_t st);
 

@@ -153,6 +153,13 @@ void ss_fill(float* ss, int C, float scale_m1, const float* shift, hipStream_t s
 __global__ void set_u64x2_kernel(uint64_t* p, uint64_t a, uint64_t b) {
   if (threadIdx.x == 0) { p[0] = a; p[1] = b; }
 }
+__global__ void stamp_init_kernel(unsigned long long* s, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) { s[2 * i] = ~0ull; s[2 * i + 1] = 0ull; }
+}
+void stamp_init(unsigned long long* s, size_t n, hipStream_t st) {
+  if (n) stamp_init_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n);
+}
 void set_u64x2(uint64_t* p, uint64_t a, uint64_t b, hipStream_t st) {
   set_u64x2_kernel<<<1, 64, 0, st>>>(p, a, b);
 }

@@ -358,7 +358,8 @@ const float* groupnorm_stats(const void* x, int B, int HW, int C, int groups, fl
                              hipStream_t st) {
   constexpr int VE = TypeInfo<T>::VE;
   const int NV = C / VE;
-  if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64) abort();   // conv_gna_ok checks this
+  if ((C / groups) % VE || NV > 256 || 256 % NV || groups > 64)   // conv_gna_ok checks this
+    throw std::invalid_argument("gn: group shape not supported");
   gn_partial<T><<<dim3(GN_CHUNKS, B), 256, 0, st>>>((const T*)x, part, HW, C, groups);
   gn_merge<<<B, 64, 0, st>>>(part, groups, eps);
   return part + (size_t)B * groups * GN_CHUNKS * 3;

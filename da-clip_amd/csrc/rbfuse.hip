@@ -117,6 +117,7 @@ bool rbfuse_ok(const RbArgs& a) {
 template <typename T, int CIN>
 __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
   kernarg_touch<sizeof(RbArgs) + 4>();                     // every kernarg line once, one wait (common.h)
+  StampGuard stamp_guard(a.stamp);                          // in-graph timing (null: off)
   using G = RBF<CIN>;
   constexpr int JT = G::JT, SW = G::SW, NC1 = G::NC1, EV = 4 * JT;
   constexpr bool FUSE = CIN == 128;
@@ -421,7 +422,7 @@ static int rbfuse_rb(const RbArgs& a, int SW) {
 
 template <typename T>
 void rbfuse(const RbArgs& a, hipStream_t st) {
-  if (!rbfuse_ok(a)) abort();
+  if (!rbfuse_ok(a)) throw std::invalid_argument("rbfuse: arguments rejected by rbfuse_ok");
   if (a.Cin == 64) {
     const int rb = rbfuse_rb(a, RBF<64>::SW);
     rbfuse_kernel<T, 64><<<a.B * (a.H / rb) * (a.W / RBF<64>::SW), 512, 0, st>>>(a, rb);

@@ -36,7 +36,8 @@ EXPORTS = ["dac_create", "dac_destroy", "dac_set_weight", "dac_finalize_weights"
            "dac_encode_image", "dac_encode_text", "dac_degradation_probs", "dac_unet_forward",
            "dac_sde_schedule", "dac_sde_set_time_scale", "dac_sde_reverse", "dac_build_id",
            "dac_set_noise_offset", "dac_posterior_step", "dac_unet_flops", "dac_encode_flops", "dac_profile_enable",
-           "dac_profile_read", "dac_op_attention", "dac_last_error"]
+           "dac_profile_read", "dac_profile_mode", "dac_profile_launch", "dac_profile_graph_ms",
+           "dac_op_attention", "dac_last_error"]
 
 
 class DacConfig(ctypes.Structure):
@@ -83,6 +84,11 @@ def lib() -> ctypes.CDLL:
         "dac_encode_flops": (D, [P, I]),
         "dac_profile_enable": (I, [P, I]),
         "dac_profile_read": (I, [P, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D)]),
+        "dac_profile_mode": (I, [P, I]),
+        "dac_profile_launch": (I, [P, I, ctypes.POINTER(D), ctypes.POINTER(D), ctypes.POINTER(D),
+                                   ctypes.POINTER(I), ctypes.POINTER(D), ctypes.POINTER(I),
+                                   ctypes.c_char_p, I, ctypes.c_char_p, I]),
+        "dac_profile_graph_ms": (I, [P, ctypes.POINTER(D)]),
         "dac_op_attention": (I, [P, P, I, I, I, I, I, P]),
         "dac_last_error": (ctypes.c_char_p, [P]),
     }

@@ -46,9 +46,23 @@ def _setup(opt: dict, device: str, dtype: str, synthetic: bool, clip_name: str):
     return model, clip, sde, s.get("sampling_mode", "posterior")
 
 
+def resolve_crop_border(opt: dict, crop_border: Optional[int] = None) -> int:
+    """The metric crop of config/daclip-sde/test.py:84, 150: `opt["crop_border"]` when set
+    (non-zero), else `opt["degradation"]["scale"]` (4 in options/test.yml:20); an explicit
+    argument overrides both. 0 means no crop (test.py:151-160)."""
+    if crop_border is not None:
+        return int(crop_border)
+    cb = opt.get("crop_border")
+    if cb:
+        return int(cb)
+    return int((opt.get("degradation") or {}).get("scale") or 0)
+
+
 def evaluate(opt: dict, lq_dir: str, gt_dir: Optional[str], out_dir: str, batch: int = 8,
              device: str = "cuda", dtype: str = "fp32", synthetic: bool = False,
-             clip_name: str = "daclip_ViT-B-32", crop_border: int = 0, suffix: str = "") -> dict:
+             clip_name: str = "daclip_ViT-B-32", crop_border: Optional[int] = None,
+             suffix: str = "") -> dict:
+    crop_border = resolve_crop_border(opt, crop_border)
     model, clip, sde, mode = _setup(opt, device, dtype, synthetic, clip_name)
     ds = LQGTDataset(lq_dir, gt_dir)
     os.makedirs(out_dir, exist_ok=True)
@@ -96,10 +110,12 @@ def main(argv=None):
     ap.add_argument("--gt", default=None)
     ap.add_argument("--out", required=True)
     ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "fp16", "bf16"])
     ap.add_argument("--synthetic", action="store_true", help="seeded synthetic weights (no checkpoints)")
     ap.add_argument("--clip", default="daclip_ViT-B-32")
-    ap.add_argument("--crop-border", type=int, default=0)
+    ap.add_argument("--crop-border", type=int, default=None,
+                    help="pixels cropped before the metrics (default: test.py:150, opt crop_border else "
+                         "degradation.scale)")
     a = ap.parse_args(argv)
     res = evaluate(parse_options(a.opt), a.lq, a.gt, a.out, a.batch, dtype=a.dtype, synthetic=a.synthetic,
                    clip_name=a.clip, crop_border=a.crop_border)

@@ -171,6 +171,21 @@ double dac_encode_flops(dac_handle* h, int B);
 int dac_profile_enable(dac_handle* h, int kernel_id);
 int dac_profile_read(dac_handle* h, double* mean_ms, double* flops_per_launch,
                      double* bytes_per_launch);
+/* graph_stamps = 1: the profiled dac_sde_reverse records its loop into a captured graph exactly
+ * as the timed loop (side-stream branches included) with a wall-clock [begin, end] stamp pair
+ * written by every launch of the class (kernel_id 999 = every conv launch), replays it once and
+ * reads each launch's in-graph duration (HIP events cannot be timed inside graph replays);
+ * 0 (default) = the eager replay with an event pair around each launch. */
+int dac_profile_mode(dac_handle* h, int graph_stamps);
+/* Launch i of the last profile (after dac_profile_read): duration (ms), algorithmic flops and
+ * bytes, conv class (kh*100 + variant), (graph mode) start time in ms after the replay's first
+ * profiled launch (-1 in eager mode), whether it ran in a concurrent branch of the UNet's split
+ * section, its shape label and (graph mode) the kernel symbol. */
+int dac_profile_launch(dac_handle* h, int i, double* ms, double* flops, double* bytes, int* kernel_class,
+                       double* start_ms, int* in_branch, char* label, int label_len, char* symbol,
+                       int symbol_len);
+/* Graph mode: HIP-event time (ms) of the profiled graph replay on the loop's stream. */
+int dac_profile_graph_ms(dac_handle* h, double* ms);
 
 /* Op-level test hook: the SpatialTransformer self-attention core on its own (the kernel
  * dac_unet_forward runs for attention.py:170-193). qkv is [B*L, 3*H*32] (q | k | v, heads

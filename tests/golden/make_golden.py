@@ -305,6 +305,80 @@ def gen_restore():
                         x_t1_sde64=seen[tuple(lq64.shape)])
 
 
+# BASELINE configs[2]'s per-GPU slice: 8 distinct real LQ photos of the reference's sample set,
+# chosen across options/test.yml:4's degradation classes by their source datasets (file names):
+MIXED_IMAGES = ["3_rain.png",                 # rainy (Rain100H-style sample, BASELINE configs[0])
+                "0048_0.9_0.2.jpg",           # hazy (RESIDE naming: id_A_beta)
+                "GOPR0871_11_00_000078.png",  # motion-blurry (GoPro)
+                "179.png",                    # low-light (LOL, 600x400)
+                "21077.png",                  # BSD-size (481x321): noisy / jpeg-compressed sets
+                "IMG_6444.jpg",               # raindrop-style capture
+                "sailing2.png",               # shadowed / inpainting sample
+                "beautiful_smile_00489.jpg"]  # face (snowy / uncompleted samples are faces too)
+MIXED_T = synth.TRACK_T
+
+
+def mixed_crops():
+    """uint8 RGB [8,256,256,3]: the 256x256 centre crop of each MIXED_IMAGES photo."""
+    from PIL import Image
+    out = []
+    for f in MIXED_IMAGES:
+        im = np.asarray(Image.open("/root/reference/images/" + f).convert("RGB"))
+        h, w = im.shape[:2]
+        y, x = (h - 256) // 2, (w - 256) // 2
+        out.append(im[y:y + 256, x:x + 256])
+    return np.ascontiguousarray(np.stack(out))
+
+
+def gen_mixed():
+    """configs[2]'s per-GPU slice pinned on real mixed inputs: the
+    reference's predict.py:58-91 flow on the 8 MIXED_IMAGES crops as ONE batch, the way
+    config/daclip-sde/test.py:102-129 feeds DenoisingModel (encode_image(control=True) ->
+    noise_state -> T=100 reverse_posterior -> tensor2img) with the restoration fixture's
+    tracking UNet weights (w_g1 / w_g2 / k of restore_rain_256_t100.npz), seed-0 ViT-B/32
+    DaCLIP, injected noise (restore_noise(tag="mx")), fp32 CPU; plus the degradation-class
+    scores softmax(100 d^ t^T) over the 10 test.yml classes and their argmax
+    (evaluate_daclip.py:45-50)."""
+    from open_clip import tokenize
+    from daclip_amd.preprocess import clip_transform
+    rgb = mixed_crops()
+    image = rgb / 255.0                                              # predict.py:64 (float64)
+    img4clip = np.stack([clip_transform(im).numpy() for im in image])
+    cfg = json.load(open(_refimport.REF + "/open_clip/model_configs/daclip_ViT-B-32.json"))
+    d = _daclip(cfg["vision_cfg"], cfg["text_cfg"], cfg["embed_dim"])
+    ic, dc = d.encode_image(T(img4clip), control=True)
+    ic, dc = ic.float(), dc.float()
+    tf = d.encode_text(tokenize(DEGRADATIONS))
+    dn = dc / dc.norm(dim=-1, keepdim=True)
+    tn = tf / tf.norm(dim=-1, keepdim=True)
+    probs = (100.0 * dn @ tn.T).softmax(dim=-1)
+    lq = torch.tensor(image, dtype=torch.float32).permute(0, 3, 1, 2).contiguous()   # predict.py:73-75
+    g = np.load(os.path.join(HERE, "restore_rain_256_t100.npz"))
+    m = ConditionalUNet(**unet_cfg(64)).eval()
+    spec = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    sd = synth.tracking_state_dict(synth.synth_state_dict(spec, 0), g["w_g1"], g["w_g2"], float(g["k"]))
+    m.load_state_dict({k: T(v) for k, v in sd.items()}, strict=True)
+    sde = ref_utils.IRSDE(max_sigma=50, T=MIXED_T, schedule="cosine", eps=0.005, device="cpu")
+    sde.set_model(m)
+    n0, steps = restore_noise(tuple(lq.shape), T=MIXED_T, tag="mx")
+    with NoiseInjector([n0]):
+        noisy = sde.noise_state(lq)
+    sde.set_mu(lq)
+    with NoiseInjector(list(steps)):
+        out = sde.reverse_posterior(noisy, text_context=dc, image_context=ic).numpy()
+    out_u8 = np.stack([ref_utils.tensor2img(T(o.copy())) for o in out])
+    lq_u8 = np.stack([ref_utils.tensor2img(T(o.copy())) for o in lq.numpy()])
+    psnr = np.array([ref_utils.calculate_psnr(a, b) for a, b in zip(out_u8, lq_u8)])
+    inr = ((out > 0) & (out < 1)).mean(axis=(1, 2, 3))
+    print(f"mixed: argmax {probs.argmax(-1).tolist()} psnr vs lq {np.round(psnr, 2).tolist()} "
+          f"in-range {np.round(inr, 4).tolist()}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "mixed8_256_t100.npz"), names=np.array(MIXED_IMAGES),
+                        classes=np.array(DEGRADATIONS), rgb_u8=rgb, img4clip=img4clip.astype(np.float32),
+                        image_context=ic.numpy(), degra_context=dc.numpy(), probs=probs.numpy(),
+                        argmax=probs.argmax(dim=-1).numpy(), out=out, out_u8=out_u8, lq_u8=lq_u8,
+                        psnr_out_vs_lq=psnr)
+
+
 def gen_variants():
     """Two sampler / context variants of the reference, 16x16 / 32x32:
     * sample_T != T: IRSDE(T=100, sample_T=50) -> 50-entry schedule and the model called at
@@ -504,7 +578,7 @@ if __name__ == "__main__":
     fns = dict(spec=gen_state_spec, unet=gen_unet_forward, sde=gen_sde, daclip=gen_daclip,
                text=gen_text, wild=gen_wild, modules=gen_modules, img=gen_img_metrics,
                headline=gen_headline, variants=gen_variants, restore=gen_restore,
-               plain=gen_plain_encode)
+               plain=gen_plain_encode, mixed=gen_mixed)
     for w in which:
         print("generating", w, flush=True)
         fns[w]()

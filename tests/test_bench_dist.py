@@ -5,6 +5,7 @@ image, noise keyed by GLOBAL image index through sde.image_offset (dac_set_noise
 the GPU), so the gathered batch must equal the single-rank batch bit for bit and every rank
 must report the same (max) time. What stays unmeasured on hardware is the RCCL leg itself
 (DESIGN.md §7)."""
+import json
 import os
 import socket
 import sys
@@ -114,3 +115,34 @@ def test_bench_step_sharded_equals_single_rank(ws):
         assert np.array_equal(out, ref), f"rank {rank}: gathered restore differs from the single-rank one"
         els.append(el)
     assert min(els) > 0 and max(els) == min(els), f"timed_steps must report the max over ranks: {els}"
+
+
+def _bench(argv, env_extra=None, timeout=240):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                          "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + argv, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` (the driver's documented form, no launcher around it) starts
+    two ranks itself; n_gpus is the process group's world size and both ranks' shards arrive
+    in the all-gather (gloo dry run: the same launcher and rank wiring, no GPU)."""
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1", "--batch", "3"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    js = lines[0]
+    assert js["n_gpus"] == 2 and js["ranks_seen"] == [0, 1] and js["global_batch"] == 6
+    assert js["steps"] == 2 and js["warmup"] == 1
+
+
+def test_bench_world_size_must_match_gpus():
+    """Under a launcher, WORLD_SIZE != --gpus is an error (never a silent 1-GPU run)."""
+    r = _bench(["--gpus", "2", "--dry-run"], dict(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in (r.stderr + r.stdout)
+    r = _bench(["--gpus", "1", "--dry-run", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1

@@ -1,4 +1,5 @@
-"""Op-level numerics of the 3x3 conv kernel family on the GPU (bf16 storage, fp32 accumulate).
+"""Op-level numerics of the 3x3 conv kernel family on the GPU (bf16 and IEEE-half storage, fp32
+accumulate).
 
 tools/convbench (built in-tree by __graft_entry__.build) runs every UNet 3x3 shape through each
 kernel choice on random inputs and compares the full output with a naive one-thread-per-output
@@ -20,10 +21,15 @@ BIN = os.path.join(ROOT, "tools", "convbench")
 
 
 @pytest.mark.gpu
-def test_conv3x3_kernels_match_naive_reference():
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+def test_conv3x3_kernels_match_naive_reference(dt):
+    """Every 3x3 kernel choice on every UNet 3x3 shape, in bf16 and in IEEE half (CB_DTYPE=f16:
+    the instantiations the fp16 headline runs), against the naive fp32 conv of the same
+    16-bit operands and a host fp64 sample."""
     assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
+    env = dict(os.environ, CB_DTYPE=dt)
     out = subprocess.run([BIN, "1", "3x3", "check", "-1,70,18,40,41,20,30,0"], capture_output=True,
-                         text=True, timeout=120, cwd=ROOT)
+                         text=True, timeout=120, cwd=ROOT, env=env)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check rel" in l]
     bad = [l for l in rows if not l.rstrip().endswith("OK")]
@@ -90,22 +96,25 @@ def test_row_phase_upsample_conv_matches_plain():
     """The UNet's Upsample convs (nearest 2x then 3x3, module_util.py:100-103) in row-phase form
     (ConvArgs::uph: output row 2i+a reads source rows (i-1, i, i) or (i, i, i+1), so its kernel
     rows fold to (W0, W1+W2) / (W0+W1, W2) and each chunk takes 2 stages instead of 3) against
-    the plain up conv with the same fp32 weights at the three UNet shapes: max-rel < 1e-2 (the
-    folded rows round to bf16 once; measured ~5e-3). Timing lines are printed."""
+    the plain up conv with the same fp32 weights at the three UNet shapes, bf16 and IEEE half:
+    max-rel < 1e-2 (the folded rows round to 16 bits once; measured ~5e-3 in bf16). Timing
+    lines are printed."""
     assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
     out = subprocess.run([BIN, "uph", "5"], capture_output=True, text=True, timeout=300, cwd=ROOT)
     print(out.stdout)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
-    assert len(rows) == 3 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+    assert len(rows) == 6 and all(l.rstrip().endswith("OK") for l in rows), out.stdout
+    assert sum(l.startswith("f16") for l in rows) == 3, out.stdout
 
 
 @pytest.mark.gpu
 def test_fused_resblock_matches_conv3r_pair():
     """The 256x256 ResBlock as one launch (rbfuse.hip: block1 3x3 + scale/shift + SiLU, block2
     3x3 + SiLU + residual, Cin 128's 1x1 res_conv too; module_util.py:115-153) against the two
-    conv3r launches it replaces, on random bf16 data: bit-identical (same ordered MFMA sums and
-    epilogue arithmetic) for one and two sources, ld2 != C2, B 1..8 and Cin 64 / 128. Timing
+    conv3r launches it replaces, on random bf16 and IEEE-half data (9 cases each): bit-identical
+    (same ordered MFMA sums and epilogue arithmetic) for one and two sources, ld2 != C2, B 1..8
+    and Cin 64 / 128. Timing
     lines (pair vs fused) are printed; the engine takes the fused form only where it pays."""
     assert os.path.exists(BIN), "tools/convbench missing: run __graft_entry__.build()"
     out = subprocess.run([BIN, "rbf", "3"], capture_output=True, text=True, timeout=300, cwd=ROOT)
@@ -113,6 +122,7 @@ def test_fused_resblock_matches_conv3r_pair():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     rows = [l for l in out.stdout.splitlines() if "check" in l]
     assert len(rows) == 18 and all(l.rstrip().endswith("check OK") for l in rows), out.stdout
+    assert sum(l.startswith("f16") for l in rows) == 9, out.stdout
 
 
 @pytest.mark.gpu

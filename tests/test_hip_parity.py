@@ -389,19 +389,24 @@ sd = synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), seed=0)
 m = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype="fp16")
 m.load_state_dict(sd)
 T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
-x = T(synth.synth_noise((4, 3, 64, 64), seed=41, tag="sp") * 0.3 + 0.5)
-mu = T(synth.synth_images(4, 64, 64, seed=42))
-tc = T(synth.synth_noise((4, 512), seed=43, tag="tc"))
-ic = T(synth.synth_noise((4, 512), seed=44, tag="ic"))
+B, R = int(sys.argv[3]), int(sys.argv[4])
+x = T(synth.synth_noise((B, 3, R, R), seed=41, tag="sp") * 0.3 + 0.5)
+mu = T(synth.synth_images(B, R, R, seed=42))
+tc = T(synth.synth_noise((B, 512), seed=43, tag="tc"))
+ic = T(synth.synth_noise((B, 512), seed=44, tag="ic"))
 np.save(sys.argv[2], m(x, mu, 37.0, text_context=tc, image_context=ic).cpu().numpy())
 """
 
 
-def test_unet_split_branches_bit_identical(tmp_path):
+@pytest.mark.parametrize("B,R,arms", [(4, 64, ("off", "two", "four")), (4, 256, ("off", "two"))])
+def test_unet_split_branches_bit_identical(tmp_path, B, R, arms):
     """The lowest levels recorded as two concurrent half-batch branches (engine.cpp
     UNetNet::section, the default DAC_SPLIT_LVL=3) against one branch (DAC_SPLIT_LVL=0), and four
-    branches of one image: bit-identical fp16 UNet outputs at B = 4, 64x64 (every kernel of the
-    section is per-image). Separate processes: the switch is read once per process."""
+    branches of one image: bit-identical fp16 UNet outputs at B = 4, 64x64 (the section covers the
+    32..8 px levels) and at 256x256, the benchmarked resolution (128..32 px: the grid-size
+    dependent choices — 3-stage ring depth, flash variants, la_apply grids — of the default
+    layout). Every kernel of the section is per-image. Separate processes: the switch is read
+    once per process."""
     import os
     import subprocess
     import sys
@@ -409,15 +414,18 @@ def test_unet_split_branches_bit_identical(tmp_path):
     script = tmp_path / "split.py"
     script.write_text(_SPLIT_SCRIPT)
     outs = {}
-    for tag, env in (("off", {"DAC_SPLIT_LVL": "0"}), ("two", {}), ("four", {"DAC_SPLIT_N": "4"})):
+    envs = {"off": {"DAC_SPLIT_LVL": "0"}, "two": {}, "four": {"DAC_SPLIT_N": "4"}}
+    for tag in arms:
+        env = envs[tag]
         e = dict(os.environ)
         e.pop("DAC_SPLIT_LVL", None)
         e.pop("DAC_SPLIT_N", None)
         e.update(env)
         path = tmp_path / f"{tag}.npy"
-        r = subprocess.run([sys.executable, str(script), root, str(path)], env=e, capture_output=True,
-                           text=True, timeout=240)
+        r = subprocess.run([sys.executable, str(script), root, str(path), str(B), str(R)], env=e,
+                           capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
         outs[tag] = np.load(path)
     assert np.isfinite(outs["off"]).all()
-    assert np.array_equal(outs["off"], outs["two"]) and np.array_equal(outs["off"], outs["four"])
+    for tag in arms[1:]:
+        assert np.array_equal(outs["off"], outs[tag]), tag

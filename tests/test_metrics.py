@@ -107,3 +107,16 @@ def test_evaluate_folder(tmp_path):
     for k in ("psnr", "ssim", "psnr_y", "ssim_y"):
         assert np.isfinite(res["summary"][k])
     assert Image.open(tmp_path / "out" / "img2.png").size == (48, 40)
+
+
+def test_evaluate_crop_border_follows_test_py():
+    """config/daclip-sde/test.py:84, 150: crop_border = opt["crop_border"] if set, else
+    opt["degradation"]["scale"] (4 in options/test.yml:20); an explicit argument wins."""
+    from daclip_amd.evaluate import resolve_crop_border
+    opt = {"degradation": {"sigma": 25, "noise_type": "G", "scale": 4}}
+    assert resolve_crop_border(opt) == 4
+    assert resolve_crop_border(dict(opt, crop_border=None)) == 4
+    assert resolve_crop_border(dict(opt, crop_border=0)) == 4            # falsy -> scale, as test.py
+    assert resolve_crop_border(dict(opt, crop_border=2)) == 2
+    assert resolve_crop_border(opt, 0) == 0
+    assert resolve_crop_border({}) == 0

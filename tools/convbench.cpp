@@ -38,15 +38,15 @@ __global__ void fill_rand_f(float* p, size_t n, uint32_t seed, float scale) {
   p[i] = ((h & 0xffff) / 65535.f - 0.5f) * scale;
 }
 // Naive reference: one thread per output element; weights [Cout][kh][kw][Cin].
-__global__ void ref_conv(ConvArgs a, int kh, int s, int p, int kws, float* out) {
+template <typename E> __global__ void ref_conv(ConvArgs a, int kh, int s, int p, int kws, float* out) {
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t M = (size_t)a.B * a.Ho * a.Wo;
   if (i >= M * a.Cout) return;
   const int n = i % a.Cout;
   const size_t m = i / a.Cout;
   const int b = m / (a.Ho * a.Wo), r = m % (a.Ho * a.Wo), oh = r / a.Wo, ow = r % a.Wo;
-  const bf16* x = (const bf16*)a.x1;
-  const bf16* w = (const bf16*)a.w;
+  const E* x = (const E*)a.x1;
+  const E* w = (const E*)a.w;
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   float acc = 0.f;
   for (int y = 0; y < kh; ++y)
@@ -54,14 +54,14 @@ __global__ void ref_conv(ConvArgs a, int kh, int s, int p, int kws, float* out) 
       const int ih = oh * s - p + y, iw = ow * s - p + z;
       if (ih < 0 || iw < 0 || ih >= Hin || iw >= Win) continue;
       const int sh = a.up ? ih >> 1 : ih, sw = a.up ? iw >> 1 : iw;
-      const bf16* xp = x + ((size_t)(b * a.Hs + sh) * a.Ws + sw) * a.ld1;
-      const bf16* wp = w + (((size_t)n * kh + y) * kws + z) * a.Cin;
+      const E* xp = x + ((size_t)(b * a.Hs + sh) * a.Ws + sw) * a.ld1;
+      const E* wp = w + (((size_t)n * kh + y) * kws + z) * a.Cin;
       for (int c = 0; c < a.Cin; ++c) acc += (float)xp[c] * (float)wp[c];
     }
   if (a.bias) acc += a.bias[n];
   if (a.ss) acc = acc * (a.ss[(size_t)b * a.ss_ld + n] + 1.f) + a.ss[(size_t)b * a.ss_ld + a.Cout + n];
   if (a.act == 1) acc = acc / (1.f + expf(-acc));
-  if (a.res1) acc += (float)((const bf16*)a.res1)[m * a.ldr1 + n];
+  if (a.res1) acc += (float)((const E*)a.res1)[m * a.ldr1 + n];
   out[i] = acc;
 }
 
@@ -84,6 +84,7 @@ static float e4m3f(uint8_t b) {
   return s ? -v : v;
 }
 static float bf2f(bf16 v) { return (float)v; }
+static float bf2f(f16 v) { return (float)v; }
 // Quantize rows of n values in 64-blocks: returns dequantized values (and e4m3 bytes + E8M0).
 static void quant_rows(const std::vector<float>& v, int rows, int n, int np, std::vector<float>& deq,
                        std::vector<uint8_t>* q8, std::vector<uint8_t>* s8) {
@@ -747,7 +748,7 @@ static int q8_check(int iters) {
 // 3x3) as two kernel rows per output-row parity with summed weights, against the plain up conv
 // with the same fp32 weights (each rounded to bf16: the folded rows round once, so the bound
 // is the bf16 rounding, max-rel < 1e-2), then both timed at B = 8.
-static int uph_check(int iters) {
+template <typename E> static int uph_check(int iters, const char* tn) {
   struct U { const char* name; int B, Hs, Ws, cin, cout; };
   const U shapes[] = {{"uph 128^2->256^2 128->64", 8, 128, 128, 128, 64},
                       {"uph 64^2->128^2 256->128", 8, 64, 64, 256, 128},
@@ -757,20 +758,20 @@ static int uph_check(int iters) {
     const int Ho = 2 * sh.Hs, Wo = 2 * sh.Ws, M = sh.B * Ho * Wo, C = sh.cin, N = sh.cout;
     uint32_t hs = 4242 + C;
     auto rnd = [&]() { hs = hs * 1664525u + 1013904223u; return ((hs >> 8) & 0xffff) / 65535.f - 0.5f; };
-    std::vector<bf16> xb((size_t)sh.B * sh.Hs * sh.Ws * C), wb((size_t)N * 9 * C), pb((size_t)N * 12 * C),
+    std::vector<E> xb((size_t)sh.B * sh.Hs * sh.Ws * C), wb((size_t)N * 9 * C), pb((size_t)N * 12 * C),
         qb((size_t)N * 16 * C);
     std::vector<float> wf((size_t)N * 9 * C), bias(N);
-    for (auto& v : xb) v = (bf16)(2.f * rnd());
+    for (auto& v : xb) v = (E)(2.f * rnd());
     for (auto& v : wf) v = 0.05f * rnd();
     for (auto& v : bias) v = 0.1f * rnd();
-    for (size_t i = 0; i < wf.size(); ++i) wb[i] = (bf16)wf[i];
+    for (size_t i = 0; i < wf.size(); ++i) wb[i] = (E)wf[i];
     const size_t R = (size_t)3 * C;
     for (int o = 0; o < N; ++o)
       for (size_t k = 0; k < R; ++k) {
         const float* w = &wf[(size_t)o * 3 * R];
-        bf16* d = &pb[(size_t)o * 4 * R];
-        d[k] = (bf16)w[k]; d[R + k] = (bf16)(w[R + k] + w[2 * R + k]);
-        d[2 * R + k] = (bf16)(w[k] + w[R + k]); d[3 * R + k] = (bf16)w[2 * R + k];
+        E* d = &pb[(size_t)o * 4 * R];
+        d[k] = (E)w[k]; d[R + k] = (E)(w[R + k] + w[2 * R + k]);
+        d[2 * R + k] = (E)(w[k] + w[R + k]); d[3 * R + k] = (E)w[2 * R + k];
       }
     {
       static const int lo[4] = {0, 1, 0, 2}, hi[4] = {0, 2, 1, 2};
@@ -781,7 +782,7 @@ static int uph_check(int iters) {
               float v = 0.f;
               for (int kh = lo[rs]; kh <= hi[rs]; ++kh)
                 for (int kw = lo[cs]; kw <= hi[cs]; ++kw) v += wf[(((size_t)o * 3 + kh) * 3 + kw) * C + c];
-              qb[(((size_t)o * 4 + rs) * 4 + cs) * C + c] = (bf16)v;
+              qb[(((size_t)o * 4 + rs) * 4 + cs) * C + c] = (E)v;
             }
     }
     void *dx, *dw, *dp, *dq, *dz, *dy0, *dy1, *dy2; float* db;
@@ -803,12 +804,12 @@ static int uph_check(int iters) {
     ConvArgs u2 = a;
     u2.w = dq; u2.K = 16 * C; u2.uph = 2; u2.y = dy2;
     const bool col = conv_uph_ok(u2);
-    if (!conv_uph_ok(u)) { printf("%-28s not eligible\n", sh.name); ++fails; continue; }
-    conv<bf16>(a, 3, 3, 1, 1, 0);
-    conv<bf16>(u, 3, 3, 1, 1, 0);
-    if (col) conv<bf16>(u2, 3, 3, 1, 1, 0);
+    if (!conv_uph_ok(u)) { printf("%s %-28s not eligible\n", tn, sh.name); ++fails; continue; }
+    conv<E>(a, 3, 3, 1, 1, 0);
+    conv<E>(u, 3, 3, 1, 1, 0);
+    if (col) conv<E>(u2, 3, 3, 1, 1, 0);
     CK(hipDeviceSynchronize());
-    std::vector<bf16> y0((size_t)M * N), y1((size_t)M * N), y2((size_t)M * N);
+    std::vector<E> y0((size_t)M * N), y1((size_t)M * N), y2((size_t)M * N);
     CK(hipMemcpy(y0.data(), dy0, y0.size() * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(y1.data(), dy1, y1.size() * 2, hipMemcpyDeviceToHost));
     if (col) CK(hipMemcpy(y2.data(), dy2, y2.size() * 2, hipMemcpyDeviceToHost));
@@ -821,9 +822,9 @@ static int uph_check(int iters) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     auto tm = [&](const ConvArgs& c) {
-      for (int i = 0; i < 3; ++i) conv<bf16>(c, 3, 3, 1, 1, 0);
+      for (int i = 0; i < 3; ++i) conv<E>(c, 3, 3, 1, 1, 0);
       CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < iters; ++i) conv<bf16>(c, 3, 3, 1, 1, 0);
+      for (int i = 0; i < iters; ++i) conv<E>(c, 3, 3, 1, 1, 0);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms = 0;
@@ -835,7 +836,7 @@ static int uph_check(int iters) {
     t1 = std::min(t1, tm(u));
     if (col) t2 = std::min(t2, tm(u2));
     const bool ok = md / mx < 1e-2 && md2 / mx < 1e-2;
-    printf("%-28s plain %6.1f us, row-phase %6.1f us, row+column %6.1f us  check rel %.2e / %.2e %s\n", sh.name, t0,
+    printf("%s %-28s plain %6.1f us, row-phase %6.1f us, row+column %6.1f us  check rel %.2e / %.2e %s\n", tn, sh.name, t0,
            t1, t2, md / mx, md2 / mx, ok ? "OK" : "FAIL");
     fails += !ok;
     for (void* p : {dx, dw, dp, dq, dz, dy0, dy1, dy2, (void*)db}) CK(hipFree(p));
@@ -1243,24 +1244,7 @@ static int c3i_st_check(int iters) {
   return bad ? 1 : 0;
 }
 
-int main(int argc, char** argv) {
-  if (argc > 1 && !strcmp(argv[1], "la")) return la_bench(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atof(argv[3]) : 0.f);
-  if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
-  if (argc > 1 && !strcmp(argv[1], "gsw")) return gsw_check(argc > 2 ? atoi(argv[2]) : 20);
-#ifdef DAC_STAMP
-  if (argc > 1 && !strcmp(argv[1], "stamp")) return stamp_check();
-#endif
-  if (argc > 1 && !strcmp(argv[1], "rbf")) {
-    const int it = argc > 2 ? atoi(argv[2]) : 20;
-    const int b = rbf_check<bf16>(it, "bf16");
-    return rbf_check<_Float16>(it, "f16 ") | b;
-  }
-  if (argc > 1 && !strcmp(argv[1], "c3r")) return c3r_check(argc > 2 ? atoi(argv[2]) : 20);
-  if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
-  if (argc > 1 && !strcmp(argv[1], "uph")) return uph_check(argc > 2 ? atoi(argv[2]) : 20);
-  if (argc > 1 && !strcmp(argv[1], "q8")) return q8_check(argc > 2 ? atoi(argv[2]) : 20);
-  if (argc > 1 && !strcmp(argv[1], "gns")) return gns_check();
-  if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
+template <typename E> static int conv_shapes(int argc, char** argv, const char* tn) {
   int iters = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 && argv[2][0] ? argv[2] : nullptr;   // substring filter
   const bool check = argc > 3 && !strcmp(argv[3], "check");
@@ -1308,20 +1292,20 @@ int main(int argc, char** argv) {
   CK(hipMemset(zero, 0, 256)); CK(hipMemset(x, 0x3c, maxe * 2)); CK(hipMemset(w, 0x3c, (size_t)4096 * 9 * 1024 * 2));
   CK(hipMemset(ss, 0, 8 * 8192 * 4)); CK(hipMemset(res, 0, maxe * 2)); CK(hipMemset(bias, 0, 8192 * 4));
   float* refo = nullptr;
-  bf16* yh = nullptr;
+  E* yh = nullptr;
   {
     // Random operands for timing too: the chip holds a lower clock on random data than on a
     // constant fill (MI355X_MICROARCH.md, DVFS give-back), so constant inputs overstate TF/s.
     const size_t nw = (size_t)4096 * 9 * 1024;
-    fill_rand<<<(maxe + 255) / 256, 256>>>((bf16*)x, maxe, 1, 2.f);
-    fill_rand<<<(nw + 255) / 256, 256>>>((bf16*)w, nw, 2, 0.1f);
-    fill_rand<<<(maxe + 255) / 256, 256>>>((bf16*)res, maxe, 3, 2.f);
+    fill_rand_t<E><<<(maxe + 255) / 256, 256>>>((E*)x, maxe, 1, 2.f);
+    fill_rand_t<E><<<(nw + 255) / 256, 256>>>((E*)w, nw, 2, 0.1f);
+    fill_rand_t<E><<<(maxe + 255) / 256, 256>>>((E*)res, maxe, 3, 2.f);
     fill_rand_f<<<(8 * 8192 + 255) / 256, 256>>>(ss, 8 * 8192, 4, 1.f);
     fill_rand_f<<<(8192 + 255) / 256, 256>>>(bias, 8192, 5, 1.f);
   }
   if (check) {
     CK(hipMalloc(&refo, maxe * 4));
-    yh = (bf16*)malloc(maxe * 2);
+    yh = (E*)malloc(maxe * 2);
   }
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto& s : shapes) for (int force : forces) {
@@ -1338,20 +1322,20 @@ int main(int argc, char** argv) {
     a.zero = zero;
     if (s.ss) { a.ss = ss; a.ss_ld = 2 * s.cout; }
     if (s.res) { a.res1 = res; a.ldr1 = s.cout; }
-    for (int i = 0; i < 3; ++i) conv<bf16>(a, s.kh, s.kh, s.s, s.p, 0);
+    for (int i = 0; i < 3; ++i) conv<E>(a, s.kh, s.kh, s.s, s.p, 0);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i) conv<bf16>(a, s.kh, s.kh, s.s, s.p, 0);
+    for (int i = 0; i < iters; ++i) conv<E>(a, s.kh, s.kh, s.s, s.p, 0);
     CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     double us = ms * 1e3 / iters;
     double fl = 2.0 * s.B * a.Ho * a.Wo * s.cout * s.kh * s.kh * s.cin;
     double by = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)s.B * a.Ho * a.Wo * s.cout * (1 + s.res));
-    printf("%-26s f%-3d variant %d  %8.1f us  %7.1f TF/s  %6.0f GB/s(min bytes)", s.name, force,
+    printf("%s%-26s f%-3d variant %d  %8.1f us  %7.1f TF/s  %6.0f GB/s(min bytes)", tn, s.name, force,
            conv_variant(a, s.kh, 2), us, fl / us / 1e6, by / us / 1e3);
     if (check) {
       const size_t n = (size_t)s.B * a.Ho * a.Wo * s.cout;
-      ref_conv<<<(n + 255) / 256, 256>>>(a, s.kh, s.s, s.p, kws, refo);
+      ref_conv<E><<<(n + 255) / 256, 256>>>(a, s.kh, s.s, s.p, kws, refo);
       CK(hipDeviceSynchronize());
       std::vector<float> r(n);
       CK(hipMemcpy(r.data(), refo, n * 4, hipMemcpyDeviceToHost));
@@ -1367,7 +1351,7 @@ int main(int argc, char** argv) {
       double hd = 0, hm = 0;
       if (s.act != 3) {
         const size_t nx = (size_t)s.B * s.H * s.W * s.cin, nw = (size_t)s.cout * a.K;
-        std::vector<bf16> hx(nx), hw(nw), hr(s.res ? n : 0);
+        std::vector<E> hx(nx), hw(nw), hr(s.res ? n : 0);
         std::vector<float> hss(s.ss ? (size_t)s.B * 2 * s.cout : 0), hb(s.bias ? s.cout : 0);
         CK(hipMemcpy(hx.data(), x, nx * 2, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hw.data(), w, nw * 2, hipMemcpyDeviceToHost));
@@ -1389,8 +1373,8 @@ int main(int argc, char** argv) {
               const int Hin = s.up ? 2 * s.H : s.H, Win = s.up ? 2 * s.W : s.W;
               if (ih < 0 || iw < 0 || ih >= Hin || iw >= Win) continue;
               const int sh = s.up ? ih >> 1 : ih, sw = s.up ? iw >> 1 : iw;
-              const bf16* xp = &hx[((size_t)(b * s.H + sh) * s.W + sw) * s.cin];
-              const bf16* wp = &hw[(((size_t)nn * s.kh + y0) * kws + z0) * s.cin];
+              const E* xp = &hx[((size_t)(b * s.H + sh) * s.W + sw) * s.cin];
+              const E* wp = &hw[(((size_t)nn * s.kh + y0) * kws + z0) * s.cin];
               for (int c = 0; c < s.cin; ++c) acc += (double)bf2f(xp[c]) * bf2f(wp[c]);
             }
           if (s.bias) acc += hb[nn];
@@ -1413,4 +1397,32 @@ int main(int argc, char** argv) {
     printf("\n");
   }
   return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "la")) return la_bench(argc > 2 ? atoi(argv[2]) : 20, argc > 3 ? atof(argv[3]) : 0.f);
+  if (argc > 1 && !strcmp(argv[1], "st")) return c3i_st_check(argc > 2 ? atoi(argv[2]) : 20);
+  if (argc > 1 && !strcmp(argv[1], "gsw")) return gsw_check(argc > 2 ? atoi(argv[2]) : 20);
+#ifdef DAC_STAMP
+  if (argc > 1 && !strcmp(argv[1], "stamp")) return stamp_check();
+#endif
+  if (argc > 1 && !strcmp(argv[1], "rbf")) {
+    const int it = argc > 2 ? atoi(argv[2]) : 20;
+    const int b = rbf_check<bf16>(it, "bf16");
+    return rbf_check<_Float16>(it, "f16 ") | b;
+  }
+  if (argc > 1 && !strcmp(argv[1], "c3r")) return c3r_check(argc > 2 ? atoi(argv[2]) : 20);
+  if (argc > 1 && !strcmp(argv[1], "fp8")) return fp8_check();
+  if (argc > 1 && !strcmp(argv[1], "uph")) {
+    const int it = argc > 2 ? atoi(argv[2]) : 20;
+    const int b = uph_check<bf16>(it, "bf16");
+    return uph_check<f16>(it, "f16 ") | b;
+  }
+  if (argc > 1 && !strcmp(argv[1], "q8")) return q8_check(argc > 2 ? atoi(argv[2]) : 20);
+  if (argc > 1 && !strcmp(argv[1], "gns")) return gns_check();
+  if (argc > 1 && !strcmp(argv[1], "lnf")) return lnf_check(argc > 2 ? atoi(argv[2]) : 20);
+  // CB_DTYPE=f16: the same shapes, kernels and checks on IEEE-half operands (the bench's
+  // headline dtype); default bf16.
+  if (getenv("CB_DTYPE") && !strcmp(getenv("CB_DTYPE"), "f16")) return conv_shapes<f16>(argc, argv, "f16 ");
+  return conv_shapes<bf16>(argc, argv, "");
 }

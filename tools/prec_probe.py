@@ -25,11 +25,23 @@ def main():
     label = sys.argv[3] if len(sys.argv) > 3 else f"{e}/{u}"
     g = np.load(os.path.join(ROOT, "tests", "golden", "restore_rain_256_t100.npz"))
     dev = torch.device("cuda", 0)
-    lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0).to(dev)
-    ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=91, tag="rs_noise_state")).to(dev)
-    zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=92, tag="rs_steps")).to(dev)
     sd = synth.tracking_state_dict(synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), 0),
                                    g["w_g1"], g["w_g2"], float(g["k"]))
+    mi = os.environ.get("PROBE_MIXED")
+    if mi is not None:
+        # image `mi` of the mixed real-image fixture (tests/golden/mixed8_256_t100.npz), with its
+        # slice of the batch's injected noise (tests/test_mixed.py mixed_noise)
+        i = int(mi)
+        m = np.load(os.path.join(ROOT, "tests", "golden", "mixed8_256_t100.npz"))
+        n0 = synth.synth_noise((8, 3, 256, 256), seed=91, tag="mx_noise_state")[i:i + 1]
+        st = synth.synth_noise((100, 8, 3, 256, 256), seed=92, tag="mx_steps")[:, i:i + 1]
+        g = {"rgb_u8": m["rgb_u8"][i], "img4clip": m["img4clip"][i:i + 1], "out": m["out"][i:i + 1],
+             "out_u8": m["out_u8"][i], "lq_u8": m["lq_u8"][i]}
+        ns, zs = torch.from_numpy(n0).to(dev), torch.from_numpy(np.ascontiguousarray(st)).to(dev)
+    lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(2, 0, 1).unsqueeze(0).to(dev)
+    if mi is None:
+        ns = torch.from_numpy(synth.synth_noise(tuple(lq.shape), seed=91, tag="rs_noise_state")).to(dev)
+        zs = torch.from_numpy(synth.synth_noise((100,) + tuple(lq.shape), seed=92, tag="rs_steps")).to(dev)
     clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, dtype=e, with_text=False)
     clip.load_synthetic(seed=0)
     unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, dtype=u)
