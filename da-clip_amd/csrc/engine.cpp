@@ -919,7 +919,12 @@ struct UNetNet {
   }
 
   // Split-precision (hi | lo) edge weights: bf16 handles (and fp8, whose activations are bf16).
-  static constexpr bool split_edges = std::is_same<T, bf16>::value;
+  // DAC_F16_EDGES=1: the same split for f16 handles (precision probe, tools/gpu_probe16.sh).
+  static bool split_edges_f() {
+    if (std::is_same<T, bf16>::value) return true;
+    static const bool f16e = sizeof(T) == 2 && getenv("DAC_F16_EDGES") && atoi(getenv("DAC_F16_EDGES")) != 0;
+    return f16e;
+  }
   void load(Packer<T>& P) {
     ss_total = cc_total = n_st = 0;
     if (degra) prompt = P.f32("prompt", {1, tdim});
@@ -931,6 +936,7 @@ struct UNetNet {
     // f16 handles keep plain weights there: f16's own weight rounding (2^-12 relative) is that of
     // the activations it produces, and the split doubles the init conv's MFMAs.
     const int kwp7 = sizeof(T) == 2 && Packer<T>::pad_to(cfg.in_nc * 2, 8) == 8 ? 8 : 0;
+    const bool split_edges = split_edges_f();
     init_conv = split_edges ? P.conv_dual("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", kwp7)
                             : P.conv("init_conv.weight", nf, cfg.in_nc * 2, 7, 7, "", false, kwp7);
     if (half) {
