@@ -54,9 +54,11 @@ def parse():
     p.add_argument("--modes", default="bf16",
                    help="comma-separated extra dtypes measured after the main line on 1 GPU (throughput "
                         "+ PSNR vs the reference), reported under 'modes'; 'none' to skip")
-    p.add_argument("--lines", default="wild-ir,fp8,fp16-b16,fp32",
+    p.add_argument("--lines", default="mixed8,wild-ir,fp8,fp16-b16,fp32",
                    help="comma-separated extra configuration lines measured after the main line on 1 GPU "
-                        "(one warmup + min(steps, 2) timed restores each), reported under 'lines': wild-ir = "
+                        "(one warmup + min(steps, 2) timed restores each), reported under 'lines': mixed8 = "
+                        "configs[2]'s per-GPU slice on 8 distinct real LQ photos with per-image dPSNR vs the "
+                        "reference run of that batch; wild-ir = "
                         "BASELINE configs[3]'s per-GPU slice (ViT-L/14 + scale-0.5 UNet, 512^2, 2 images), fp8 = "
                         "configs[4]'s per-GPU slice (256^2, 16 images, e4m3 GEMMs), fp16-b16 = the same 16 images in "
                         "fp16 (equal-batch comparison for fp8), fp32 = the parity mode on the main workload; "
@@ -588,6 +590,63 @@ LINES = {
 }
 
 
+def mixed_line(args, dev):
+    """BASELINE configs[2]'s per-GPU slice on REAL inputs: the 8 distinct LQ photos of
+    tests/golden/mixed8_256_t100.npz (rain, haze, motion blur, low light, ... 256x256 crops of the
+    reference's sample images) as one B=8 batch in the benchmarked dtype, with the restoration
+    fixture's tracking UNet weights (synth.tracking_state_dict) and seed-0 ViT-B/32. Throughput:
+    the same step as the main line (encode -> noise_state -> graph loop, device noise), one warmup
+    and min(steps, 2) timed restores. Parity: one more restore with the fixture's injected noise,
+    every image's dPSNR against the reference's run of the same batch, and the degradation-class
+    argmax (text tower on this GPU) against the reference's."""
+    from daclip_amd import arch, synth
+    from daclip_amd.unet import ConditionalUNet
+    from daclip_amd.open_clip import DaCLIP
+    from daclip_amd.sde import IRSDE
+    from daclip_amd.preprocess import tensor2img, calculate_psnr
+    t0 = time.perf_counter()
+    gd = os.path.join(ROOT, "tests", "golden")
+    g = np.load(os.path.join(gd, "mixed8_256_t100.npz"))
+    r = np.load(os.path.join(gd, "restore_rain_256_t100.npz"))
+    sd = synth.tracking_state_dict(synth.synth_state_dict(arch.unet_state_spec(arch.UNetConfig()), 0),
+                                   r["w_g1"], r["w_g2"], float(r["k"]))
+    unet = ConditionalUNet(3, 3, 64, [1, 2, 4, 8], 512, True, True, device=dev, dtype=args.dtype)
+    unet.load_state_dict(sd)
+    clip = DaCLIP(arch.VIT_B_32, arch.TEXT_B_32, device=dev, dtype=args.dtype)
+    clip.load_synthetic(seed=0)
+    sde = IRSDE(max_sigma=50, T=100, schedule="cosine", eps=0.005)
+    sde.set_model(unet)
+    lq = torch.tensor(g["rgb_u8"] / 255.0, dtype=torch.float32).permute(0, 3, 1, 2).contiguous().to(dev)
+    img = torch.from_numpy(g["img4clip"]).to(dev)
+    B = lq.shape[0]
+    k = min(args.steps, 2)
+    out, el = timed_steps(make_step(clip, sde, lq, img, 0, B, 1), 1, k, 1, dev)
+    res = {"line": "mixed8", "config": "configs[2] per-GPU slice on real inputs: 8 distinct LQ photos "
+                                       "(tests/golden/mixed8_256_t100.npz), 256x256, one batch",
+           "images": [str(x) for x in g["names"]], "dtype": args.dtype, "batch_per_gpu": B,
+           "value": round(B * k / el, 4), "unit": "images/s", "ms_per_step": round(el / k * 1e3, 2), "steps": k,
+           "outputs_finite": bool(torch.isfinite(out).all().item())}
+    if not args.no_psnr:
+        shape = (B, 3, 256, 256)
+        n0 = torch.from_numpy(synth.synth_noise(shape, seed=91, tag="mx_noise_state")).to(dev)
+        zs = torch.from_numpy(synth.synth_noise((100,) + shape, seed=92, tag="mx_steps")).to(dev)
+        ic, dc = clip.encode_image(img, control=True)
+        t = np.load(os.path.join(gd, "text_b32.npz"))
+        _, am = clip.degradation_probs(dc, clip.encode_text(torch.from_numpy(t["tokens"])))
+        sde.set_mu(lq)
+        o = sde.reverse_posterior(sde.noise_state(lq, noise=n0), noises=zs, text_context=dc, image_context=ic)
+        o = o.cpu()
+        d = [float(calculate_psnr(tensor2img(o[b]), g["lq_u8"][b]) - calculate_psnr(g["out_u8"][b], g["lq_u8"][b]))
+             for b in range(B)]
+        res["psnr"] = {"vs": "reference CPU path on the same batch (make_golden.py gen_mixed)",
+                       "delta_db": [round(x, 6) for x in d], "max_abs_delta_db": round(max(map(abs, d)), 6),
+                       "mean_delta_db": round(float(np.mean(d)), 6),
+                       "argmax": am.cpu().numpy().tolist(), "argmax_equals_reference":
+                           bool(np.array_equal(am.cpu().numpy(), g["argmax"]))}
+    res["wall_s"] = round(time.perf_counter() - t0, 1)
+    return res
+
+
 def extra_line(args, name, dev):
     """One more BASELINE configuration on this GPU (driver-observed in the same run): its own
     handles with the seeded synthetic weights, the same step as the main line (encode ->
@@ -740,8 +799,11 @@ def main():
         if ws == 1 and args.model == "universal-ir" and lines:
             res["lines"] = []
             for x in lines:
+                if x == "mixed8":
+                    res["lines"].append(mixed_line(args, dev))
+                    continue
                 if x not in LINES:
-                    raise SystemExit(f"bench: unknown line {x!r} (choose from {sorted(LINES)})")
+                    raise SystemExit(f"bench: unknown line {x!r} (choose from {sorted(LINES) + ['mixed8']})")
                 if LINES[x][3] == args.dtype and LINES[x][1] == args.res and LINES[x][2] == args.batch:
                     continue                       # that is the main line itself
                 res["lines"].append(extra_line(args, x, dev))

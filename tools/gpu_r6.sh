@@ -23,4 +23,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 grep '^{' $O/profrun.log > $O/bench_under_prof.json
 python3 tools/kstats.py $(find $O/prof -name "*kernel_stats.csv" | head -1) > $O/kernel_stats_summary.txt
 head -25 $O/kernel_stats_summary.txt | cut -c1-160
+if [ "${3:-}" = full ]; then
+  timeout -k 10 900 python -u bench.py > $O/bench.log 2>&1 || { echo FULL BENCH FAILED; tail -20 $O/bench.log; exit 1; }
+  grep '^{' $O/bench.log > $O/bench.json
+  cut -c1-800 $O/bench.json
+fi
 exit ${rc:-0}
