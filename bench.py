@@ -506,6 +506,9 @@ def dominant_roofline(h, step, dtype, step_ms, pmc_ok=False, eager=True):
     rows, graph_ms, prof_step_ms = graph_profile(h, step)
     if not rows:
         return None
+    if os.environ.get("BENCH_PROFILE_DUMP"):          # per-launch rows for offline analysis
+        with open(os.environ["BENCH_PROFILE_DUMP"], "w") as f:
+            json.dump({"graph_ms": graph_ms, "rows": rows}, f)
     peak = MFMA_PEAK[dtype]
     shares = time_shares(rows)
     syms = _group(rows, lambda c, s: s or f"class {c}", shares)

@@ -213,6 +213,25 @@ int conv_split_k(const ConvArgs& a, int elem_bytes, long rows) {
   return s >= 2 ? s : 0;
 }
 
+bool conv3_split_ok(const ConvArgs& a, int elem_bytes) {
+  const int VEh = 16 / elem_bytes, BKE = 128 / elem_bytes;
+  if (a.y2 || a.w2 || a.up || a.uph || a.ys8 || a.xs8 || a.cwrap || a.w_bstride || a.amode || a.ln_g ||
+      a.lnf_cs || a.gna_stats || !a.zero)
+    return false;
+  if (a.act != ACT_NONE && a.act != ACT_SILU) return false;
+  if (a.Cin % BKE || a.Cout % VEh || a.ldy % VEh || a.Cout <= 16) return false;
+  if (a.Ho != a.Hs || a.Wo != a.Ws || a.K != 9 * a.Cin) return false;
+  if (a.x2 && a.C1 % BKE) return false;
+  return conv3_rw_host(a, 128) > 0 && conv3_rw_host(a, 256) > 0;
+}
+
+int conv3_split_k(const ConvArgs& a, int elem_bytes, int ks) {
+  if (ks < 2 || !conv3_split_ok(a, elem_bytes)) return 0;
+  const int nchunk = a.Cin / (128 / elem_bytes);
+  while (ks > 1 && nchunk / ks < 2) --ks;
+  return ks >= 2 ? ks : 0;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) conv_part_reduce_kernel(ConvArgs a, int M, size_t n) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;

@@ -1034,10 +1034,17 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
+  // Split-K (ConvArgs::ksplit > 1, grid z = ksplit): this block sums the Cin chunks of split
+  // tl.bz only and writes raw fp32 partials; conv_part_reduce adds the splits in order and
+  // applies the epilogue. The split count comes from one image's shape (engine conv_call), so an
+  // image's summation order never depends on the batch.
+  const bool part = a.ksplit > 1;
+  const int c_lo = part ? (int)((long)tl.bz * nchunk / a.ksplit) : 0;
+  const int c_hi = part ? (int)((long)(tl.bz + 1) * nchunk / a.ksplit) : nchunk;
   // Stages s = 3c + kh alternate buffers; kh is unrolled so the A source table index is static.
-  issue(0, 0, 0);
+  issue(c_lo, 0, 0);
   int buf = 0;
-  for (int c = 0; c < nchunk; ++c) {
+  for (int c = c_lo; c < c_hi; ++c) {
     sync_stage();
     issue(c, 1, buf ^ 1);
     compute(buf);
@@ -1047,7 +1054,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
     compute(buf);
     buf ^= 1;
     sync_stage();
-    if (c + 1 < nchunk) issue(c + 1, 0, buf ^ 1);
+    if (c + 1 < c_hi) issue(c + 1, 0, buf ^ 1);
     compute(buf);
     buf ^= 1;
   }
@@ -1057,6 +1064,21 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const Rows rm{b * HWo + oh0 * a.Wo + ow0, rws, a.Wo};
+  if (part) {
+    // Tile i row 4 lg + r is block pixel t (rm(t) in the image), column lr of tile jn is channel n.
+    const size_t M = (size_t)a.B * HWo;
+    float* pz = a.part + (size_t)tl.bz * M * a.Cout;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = wm * WTM + i * 16 + 4 * lg + r, n = n0 + wn * WTN + jn * 16 + lr;
+          if (n < a.Cout) pz[(size_t)rm(t) * a.Cout + n] = acc[i][jn][r];
+        }
+    return;
+  }
   conv_epilogue_lds<T, BM, BN, WGM, WGN, EPR, EPI_MIN>(a, acc, smem, (b + 1) * HWo, rm, n0, HWo, b, &et);
 }
 
@@ -2164,6 +2186,17 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
   // (init conv Cin=8, patch embed, final conv Cout=3, LinearAttention to_out amode=1).
   constexpr bool V2 = (KH == 1 || KH == 3 || KH == 4);
   const bool v2ok = V2 && a.zero != nullptr && a.Cin % BKE == 0 && a.amode == 0 && a.Cout > 16;
+  if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
+    if (a.ksplit > 1 && a.part) {
+      // Split-K (engine conv_call; conv3_split_ok): v3's 8-wave 128 x 128 form over ksplit Cin
+      // ranges (grid z), then the in-order reduce + epilogue pass.
+      if (!conv3_split_ok(a, (int)sizeof(T))) throw std::invalid_argument("conv: 3x3 split-K on a shape without it");
+      dim3 g(a.B * a.Ho * a.Wo / 128, (a.Cout + 127) / 128, a.ksplit);
+      conv3_launch<T, 128, 128, 4, 2, 128>(a, g, conv3_rw(a, 128), st);
+      conv_part_reduce<T>(a, st);
+      return;
+    }
+  }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2) {
     if (g_conv3_force < 0 && conv3n_ok(a)) {   // final_conv: conv_edge.hip
       conv3n<T>(a, st);

@@ -26,6 +26,17 @@ static int env_mask(const char* n) {
   return v ? (int)strtol(v, nullptr, 0) : 0;
 }
 static int emu_w() { static const int m = env_mask("DAC_EMU_W"); return m; }
+// Per-image split-K count for the 3x3 convs (and split-K for the 1x1 GEMMs) of the UNet levels of
+// at most 1024 pixels per image (the 32x32 level at 256^2), set by UNetNet::forward from the
+// handle's policy: Wild-IR (scale-0.5) handles, whose configs[3] slice is 2 images per GPU, use 4;
+// the universal handles none (DAC_SPLITK32=k overrides both; 0 = off). A function of the
+// network, never of the batch: an image's summation order is the same in every batch / shard.
+static thread_local int g_splitk = 0;
+struct SplitKScope {
+  int prev;
+  explicit SplitKScope(int k) : prev(g_splitk) { g_splitk = k; }
+  ~SplitKScope() { g_splitk = prev; }
+};
 static int emu_a() { static const int m = env_mask("DAC_EMU_A"); return m; }
 static thread_local int g_role = R_OTHER;
 struct RoleScope {
@@ -623,9 +634,19 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   }
   Profiler* p = r.prof;
   const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
+  // Per-image split-K at the small levels (g_splitk, UNetNet::forward): 3x3 convs over ks Cin
+  // ranges; the count depends on one image's shape and the handle's policy, never on B.
+  int ks3 = 0;
+  if (g_splitk > 1 && cw.kh == 3 && cw.kw == 3 && stride == 1 && pad == 1 && !up && !use8 && !a.uph &&
+      (long)a.Ho * a.Wo <= 1024 && a.Ho > 1) {
+    ConvArgs q = a;
+    q.w2 = nullptr; q.bias2 = nullptr; q.y2 = nullptr; q.w2_dual = 0; q.ldy2 = 0;
+    if (!r.zero) q.zero = &q;
+    ks3 = conv3_split_k(q, (int)sizeof(T), g_splitk);
+  }
   bool fused = false;
   if (e.fuse1x1) {
-    fused = sizeof(T) == 2 && !use8 && a.w2 && cw.kh == 3 && stride == 1 && pad == 1 && !up &&
+    fused = sizeof(T) == 2 && !use8 && !ks3 && a.w2 && cw.kh == 3 && stride == 1 && pad == 1 && !up &&
             e.fuse1x1->cout == cw.cout && e.fuse1x1->cin == cw.cin && conv_res_fusable(a);
     if (!fused) {
       a.w2 = nullptr; a.bias2 = nullptr; a.y2 = nullptr; a.w2_dual = 0; a.ldy2 = 0;
@@ -635,11 +656,19 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
       fl += 2.0 * M * cw.cout * e.fuse1x1->cin_real;
     }
   }
-  // Split-K (the small-M 1x1 GEMMs: ViT / text tower linears): fp32 partials from the arena.
-  if (e.split_rows > 0 && cw.kh == 1 && cw.kw == 1 && stride == 1 && pad == 0 && !use8 && !e.fuse1x1) {
+  if (ks3 > 1) {
+    a.ksplit = ks3;
+    a.part = r.alloc<float>((size_t)ks3 * (size_t)M * cw.cout);
+  }
+  // Split-K (the small-M 1x1 GEMMs: ViT / text tower linears, and the UNet's small levels under
+  // g_splitk): fp32 partials from the arena; the count follows one image's rows.
+  static const bool split1 = !getenv("DAC_SPLITK32_1X1") || atoi(getenv("DAC_SPLITK32_1X1")) != 0;
+  const long srows = e.split_rows > 0 ? e.split_rows
+                     : (split1 && g_splitk > 1 && a.Ho > 1 && a.Wo > 1 && (long)a.Ho * a.Wo <= 1024) ? (long)a.Ho * a.Wo : 0;
+  if (srows > 0 && cw.kh == 1 && cw.kw == 1 && stride == 1 && pad == 0 && !use8 && !e.fuse1x1) {
     ConvArgs q = a;
     if (!r.zero) q.zero = &q;
-    const int ks = conv_split_k(q, (int)sizeof(T), e.split_rows);
+    const int ks = conv_split_k(q, (int)sizeof(T), srows);
     if (ks > 1) {
       a.ksplit = ks;
       a.part = r.alloc<float>((size_t)ks * (size_t)M * cw.cout);
@@ -1446,6 +1475,8 @@ struct UNetNet {
     // Roles are assigned per section below; this scope restores the caller's role when the
     // forward returns (ViT / encoder calls on the thread are unaffected).
     RoleScope rs_init(R_INIT);
+    static const int splitk_env = getenv("DAC_SPLITK32") ? atoi(getenv("DAC_SPLITK32")) : -1;
+    SplitKScope sks(splitk_env >= 0 ? splitk_env : (half ? 4 : 0));
     conv_call<T>(r, init_conv, xin, 8, 8, nullptr, 0, B, Hp, Wp, 0, 1, 3, x0, nf, Epi());
     std::vector<std::pair<const void*, int>> hs;
     const void* cur = x0;

@@ -201,6 +201,11 @@ bool conv_q8out_ok(const ConvArgs& a);
 // Split-K (ConvArgs::ksplit / part): the 1x1 GEMM this engine call would split, and its second
 // pass (sum of the ksplit partials in order, then bias -> scale/shift -> activation -> residuals).
 int conv_split_k(const ConvArgs& a, int elem_bytes, long rows);
+// 3x3 (stride 1, pad 1) split-K: the v3 form can take this conv with ksplit > 1 (plain
+// epilogues: bias, scale/shift, SiLU, residuals; no fused res_conv, upsampling, fp8 or phases).
+bool conv3_split_ok(const ConvArgs& a, int elem_bytes);
+// Split count of such a conv from ONE image's shape: `ks` Cin ranges of >= 2 chunks each.
+int conv3_split_k(const ConvArgs& a, int elem_bytes, int ks);
 template <typename T>
 void conv_part_reduce(const ConvArgs& a, hipStream_t st);
 // Row-phase upsample conv (ConvArgs::uph): the dispatcher has the kernel for this conv.
