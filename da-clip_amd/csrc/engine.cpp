@@ -636,9 +636,10 @@ void conv_call(Run& r, const ConvW& cw, const void* x1, int ld1, int C1, const v
   const bool use8 = sizeof(T) == 2 && cw.w8 && conv8_ok(a, cw.kh, cw.kw, stride, pad);
   // Per-image split-K at the small levels (g_splitk, UNetNet::forward): 3x3 convs over ks Cin
   // ranges; the count depends on one image's shape and the handle's policy, never on B.
+  static const long split_px = getenv("DAC_SPLITK_PX") ? atol(getenv("DAC_SPLITK_PX")) : 1024;
   int ks3 = 0;
   if (g_splitk > 1 && cw.kh == 3 && cw.kw == 3 && stride == 1 && pad == 1 && !up && !use8 && !a.uph &&
-      (long)a.Ho * a.Wo <= 1024 && a.Ho > 1) {
+      (long)a.Ho * a.Wo <= split_px && a.Ho > 1) {
     ConvArgs q = a;
     q.w2 = nullptr; q.bias2 = nullptr; q.y2 = nullptr; q.w2_dual = 0; q.ldy2 = 0;
     if (!r.zero) q.zero = &q;
