@@ -79,7 +79,7 @@ template <typename T> DEV void st_lds(char* p, const float* v, int n) {
 }
 }  // namespace
 
-// DAC_RBFUSE: 0 off, 1 (default) where it pays (rbfuse_pays), 2 wherever it applies (A/B runs).
+// DAC_RBFUSE: 0 off, 1 (default) / 2 wherever it applies, 3 the round-5 rule (rbfuse_pays).
 static int g_rbfuse_on = getenv("DAC_RBFUSE") ? atoi(getenv("DAC_RBFUSE")) : 1;
 extern "C" void dac_rbfuse_enable(int on) { g_rbfuse_on = on; }
 
@@ -94,11 +94,15 @@ extern "C" void dac_rbfuse_enable(int on) { g_rbfuse_on = on; }
 // every image's output unchanged (tests/test_hip_parity.py batch tests).
 // In the network (rocprof, fp16 bench, B = 8) the 64 -> 64 fused block beats the pair too — 91.4
 // against 45.6 + 48.8 us, its cold-input reads cost the pair more than convbench's warm L2 shows —
-// while the Cin 128 form stays behind (153.1 against 91.4 + 48.8 us). So Cin 64 always, Cin 128 up
-// to two images.
+// while the Cin 128 form stayed behind in round 5 (153.1 against 91.4 + 48.8 us). Round 6, whole
+// bench A/B with the current kernels (tools/gpu_ab.sh rbf2 / rbf2b, 8 interleaved pairs on two
+// boxes): the Cin 128 form at 8 images too is +0.6 % images/s (27.70 -> 27.85 mean; every pair >=),
+// so it now takes every ResBlock it applies to. DAC_RBFUSE=3 restores the round-5 rule (Cin 64
+// always, Cin 128 up to two images) for A/B runs.
 bool rbfuse_pays(const RbArgs& a) {
   const size_t px = (size_t)a.B * a.H * a.W, img = (size_t)256 * 256;
-  return g_rbfuse_on == 2 || a.Cin == 64 || px <= 2 * img;
+  if (g_rbfuse_on == 3) return a.Cin == 64 || px <= 2 * img;
+  return true;
 }
 
 bool rbfuse_ok(const RbArgs& a) {
