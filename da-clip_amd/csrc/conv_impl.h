@@ -857,9 +857,12 @@ inline int conv3_rw(const ConvArgs& a, int BM = 256) {
 }
 
 // CK = bytes of one LDS row (one K chunk of one pixel): 128 (8 slots) or 64 (4 slots). A
-// wave-instruction of global_load_lds fills 64 / SLOTS rows; slot swizzle sl ^ f(row) with
-// f(row) = (row >> log2(16 / SLOTS)) & (SLOTS - 1) keeps the 16 rows read by one ds_read_b128
-// lane group on distinct banks.
+// wave-instruction of global_load_lds fills 64 / SLOTS rows; slot swizzle sl ^ f(row). An A
+// fragment's 16 rows start at any row (the kw tap shifts them by 0..2 and output rows start at
+// oy * (RW + 2)), so f must keep every ds_read_b128 lane group ({0-3,12-15,20-27}, ...) on
+// distinct bank quads for odd starts too: f = row & 7 (8 slots) and ((row >> 2) & 1) * 2 (4 slots)
+// do, found by enumerating the lane groups over every start (the earlier (row >> 1) & 7 was
+// 2-way on odd starts: SQ_LDS_BANK_CONFLICT 17.8% of LDS cycles on the 512-channel 32² conv).
 // BUF: buffer-descriptor DMA (as v4 FL bit 10): per-lane 32-bit offsets computed once, the chunk
 // and kh advance in the scalar soffset, padding as out-of-range offsets -- no 64-bit address
 // arithmetic per DMA instruction (v3 spent ~3 VALU per MFMA there). One row pitch required.
@@ -871,7 +874,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   constexpr int VE = TypeInfo<T>::VE;
   constexpr int ES = sizeof(T);
   constexpr int BKE = CK / ES;
-  constexpr int SLOTS = CK / 16, RPI = 64 / SLOTS, SSH = SLOTS == 8 ? 1 : 2;
+  constexpr int SLOTS = CK / 16, RPI = 64 / SLOTS;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int NPIX_MAX = BM + 2 * (BM / 16);           // RH * (RW + 2) with RW >= 16
@@ -901,7 +904,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
   const int Hin = a.up ? 2 * a.Hs : a.Hs, Win = a.up ? 2 * a.Ws : a.Ws;
   const char* zero = reinterpret_cast<const char*>(a.zero);
   const int pixb = b * a.Hs * a.Ws;
-  auto fsw = [](int row) { return (row >> SSH) & (SLOTS - 1); };
+  auto fsw = [](int row) { return SLOTS == 8 ? row & 7 : ((row >> 2) & 1) << 1; };
 
   // Per lane and A row j: source pixel index for each kh (-1 = padding) and the 16-byte slot
   // it fills (source-side swizzle).

@@ -312,10 +312,19 @@ struct LaCfg {
   static constexpr int QV = C / 4 / VE;                  // x vectors per thread (4 thr / px)
   static constexpr bool WREG = ES == 2 && C <= 128;      // weights cached in registers (C = 256: L2)
   static constexpr int SMEM = 2 * XT + 4 * 64 * 4;      // x tiles + per-wave rescale scratch
-  DEV static int swz(int row, int s) {                   // x tile slot swizzle
-    const int f = SL >= 16 ? (row & 15) : SL == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
+  // x tile slot swizzle and the slot of loader vector j of thread qq (4 threads per pixel). Both
+  // sides have to be conflict-free: the {lr, lg} ds_read_b128 fragment reads (16 rows from a
+  // multiple of 16) and the ds_write_b128 stores (8 lanes = 2 pixels x 4 threads per group, banks
+  // mod 32). 16-bit tiles: 128-byte rows f = row & 7 with vectors qq*QV + j; 256/512-byte rows
+  // f = 6 row mod SL with vectors j*4 + qq (found by enumerating both patterns; the earlier
+  // (row >> 1) & 7 and row & 15 stored 2-way (C = 64, 128) and 4-way (C = 256) conflicted:
+  // SQ_LDS_BANK_CONFLICT 20 % / 21 % / 47 % of the LDS cycles).
+  DEV static int swz(int row, int s) {
+    const int f = ES == 2 ? (SL == 8 ? (row & 7) : ((row * 6) & (SL - 1)))
+                          : SL >= 16 ? (row & 15) : SL == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
     return row * RB + ((s ^ f) << 4);
   }
+  DEV static int vslot(int qq, int j) { return ES == 2 && SL >= 16 ? j * 4 + qq : qq * QV + j; }
 };
 
 // 16 bytes of MFMA operand (8 bf16 or 4 f32) assembled element by element.
@@ -379,7 +388,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
     const int p = t0 + lp;
 #pragma unroll
     for (int j = 0; j < K::QV; ++j)
-      xr[j] = (lp < TP && p < p1) ? *reinterpret_cast<const u32x4*>(xb + (size_t)p * C + (qq * K::QV + j) * VE)
+      xr[j] = (lp < TP && p < p1) ? *reinterpret_cast<const u32x4*>(xb + (size_t)p * C + K::vslot(qq, j) * VE)
                                   : u32x4{0u, 0u, 0u, 0u};
   };
   // LayerNorm of the loaded pixel (two-pass in registers, like ln_kernel) -> LDS tile. The
@@ -411,7 +420,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(C == 6
       float o[VE];
 #pragma unroll
       for (int i = 0; i < VE; ++i) o[i] = (v[j][i] - mean) * rstd;
-      store_vec<T>(reinterpret_cast<T*>(dst + K::swz(lp, qq * K::QV + j)), o);
+      store_vec<T>(reinterpret_cast<T*>(dst + K::swz(lp, K::vslot(qq, j))), o);
     }
   };
 
@@ -727,16 +736,17 @@ __global__ void __launch_bounds__(256) la_apply(const T* __restrict__ x, const T
   constexpr int KS = C / KSTEP;                           // q-projection k-steps
   constexpr int KO = 128 / KSTEP;                         // out-GEMM k-steps
   constexpr int NH = C / 64;                              // 64-channel output halves
-  // LDS rows: 128- and 256-byte rows use an XOR slot swizzle (bank-conflict free for the
+  // LDS rows: 128-, 256- and 512-byte rows use an XOR slot swizzle (bank-conflict free for the
   // {lr, lg} fragment reads: the +16 B padding it replaced was 2-way conflicted, 35 % of the
-  // LDS cycles); wider (fp32) rows keep the padding.
+  // LDS cycles, and still 22 % on the C = 256 Wq rows until those took the swizzle too); wider
+  // (fp32) rows keep the padding.
   constexpr int QRB = C * ES, ERB = 128 * ES;
-  constexpr int WROW = (QRB == 128 || QRB == 256) ? QRB : QRB + 16;
+  constexpr int WROW = (QRB == 128 || QRB == 256 || QRB == 512) ? QRB : QRB + 16;
   constexpr int EROW = (ERB == 128 || ERB == 256) ? ERB : ERB + 16;
   constexpr int SMEM = 128 * WROW + C * EROW + 2 * C * 4;
   auto qoff = [](int row, int slot) {
     if constexpr (QRB == 128) return row * 128 + ((slot ^ ((row >> 1) & 7)) << 4);
-    else if constexpr (QRB == 256) return row * 256 + ((slot ^ (row & 15)) << 4);
+    else if constexpr (QRB == 256 || QRB == 512) return row * QRB + ((slot ^ (row & 15)) << 4);
     else return row * WROW + (slot << 4);
   };
   auto eoff = [](int row, int slot) {
