@@ -191,10 +191,7 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
   };
   const int bq0 = quad_base(0), bq1 = quad_base(1);
   // Fragment offset of halo pixel 64 g + 4 lr + s (s = 0 .. 7) and chunk parity c, from the two
-  // quad bases as (re)defined per fragment group: the bases pass through an empty asm at each
-  // group, so the compiler derives the six offsets there instead of hoisting all twelve (and the
-  // edge tile's) into registers for the kernel's lifetime (they spilled: VGPRs are the limit).
-  auto fresh = [](int v) { asm volatile("" : "+v"(v)); return v; };
+  // quad bases (each conv precomputes the twelve it reads).
   auto foff = [&](int b0, int b1, int s, int c) {
     const int base = s < 4 ? b0 : b1;              // (s < 8)
     return base ^ ((s & 3) << 7) ^ (c << 6);
@@ -222,6 +219,18 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
     issue_x(r0 - 2);
     issue_x(r0 - 1);
     issue_x(r0);
+    // Fragment offsets within a ring row, computed once: the six interior ones per chunk parity
+    // and the edge tile's three (per kw). Re-deriving them per fragment group (to save VGPRs)
+    // cost 390 VALU per step beside 180 MFMAs at Cin 128 (the edge tile's select / swizzle chain
+    // alone ~9 per read); held, they take the kernels to 224 (Cin 128) / 250 (Cin 64) of the 256
+    // VGPRs two waves per SIMD allow, with no scratch.
+    int eoff[3], fo[2][6];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) eoff[kw] = rbf_off(lr < 8 ? SW + 1 + kw : kw, lg);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) fo[c][s] = foff(bq0, bq1, s + 1, c);
     for (int st = 0; st < nsteps; ++st) {
       const int t = r0 - 1 + st;
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // x row t + 1 landed; h writes done
@@ -248,10 +257,9 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
           __builtin_amdgcn_sched_barrier(0);
           const char* hr = xr + (c32 >> 1) * G::XHALF;
           const int c = c32 & 1;
-          const int b0 = fresh(bq0), b1 = fresh(bq1);
           u32x4 F[6];
 #pragma unroll
-          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, s + 1, c));
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + fo[c][s]);
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -259,10 +267,9 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
 #pragma unroll
               for (int j = 0; j < JT; ++j) Mma<T>::run(acc[i][j], W[(kh * 3 + kw) * NC1 + c32][j], F[i + kw]);
           {
-            const int le = fresh(lr);
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
-              const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (rbf_off(le < 8 ? SW + 1 + kw : kw, lg) ^ (c << 6)));
+              const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (eoff[kw] ^ (c << 6)));
               if (JT == 1 || g == 0) Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][0], E);
               else Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][JT - 1], E);
             }
@@ -327,7 +334,13 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
     T* y = reinterpret_cast<T*>(a.y);
-    const int q16 = nb >> 3, half8 = (nb >> 2) & 1;
+    const int q16 = nb >> 3;
+    // Interior fragment offsets per chunk parity, once (block2's waves have the VGPRs to spare).
+    int fo[2][6];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int s = 0; s < 6; ++s) fo[c][s] = foff(bq0, bq1, s, c);
     for (int st = 0; st < nsteps; ++st) {
       const int t = r0 - 1 + st, u = t - 2;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -345,10 +358,9 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           __builtin_amdgcn_sched_barrier(0);
-          const int b0 = fresh(bq0), b1 = fresh(bq1);
           u32x4 F[6];
 #pragma unroll
-          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, s, c));
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + fo[c][s]);
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -370,11 +382,10 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
 #pragma unroll
         for (int c32 = 0; c32 < NC1; ++c32) {
           __builtin_amdgcn_sched_barrier(0);
-          const int b0 = fresh(bq0), b1 = fresh(bq1);
           const char* hr = xr + (c32 >> 1) * G::XHALF;
           u32x4 F[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) F[i] = *reinterpret_cast<const u32x4*>(hr + foff(b0, b1, i + 2, c32 & 1));
+          for (int i = 0; i < 4; ++i) F[i] = *reinterpret_cast<const u32x4*>(hr + fo[c32 & 1][i + 2]);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
