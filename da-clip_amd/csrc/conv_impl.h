@@ -733,6 +733,10 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
 #pragma unroll
           for (int i = 0; i < TM; ++i) lsh[i] = to_f(*reinterpret_cast<const T*>(A + swz(wm * WTM + i * 16 + lr, 0)));
         }
+        // The WGN waves of a row band read the same A fragments: each takes the moments of its
+        // share of the k-steps (ks % WGN == wn; 8 VALU per fragment word made this loop VALU-bound
+        // at 2x its MFMA time) and the shares are summed after the loop.
+        if (WGN > 1 && ks % WGN != __builtin_amdgcn_readfirstlane(wn)) continue;   // (wave-uniform)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -750,6 +754,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   DAC_ST(3, __builtin_amdgcn_s_memtime());
   if constexpr (LNF) {
+    if constexpr (WGN > 1) {
+      // Sum the WGN waves' k-step shares per lane, in wave order (every wave of the band forms the
+      // same sums), through LDS: the K loop's reads are done after this barrier.
+      static_assert(WGN * 2 * TM * 64 * 4 * WGM <= STAGES * STAGE, "LN-fold exchange fits the pipeline LDS");
+      float* xm = reinterpret_cast<float*>(smem);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        xm[((wave * TM + i) * 2) * 64 + lane] = ls1[i];
+        xm[((wave * TM + i) * 2 + 1) * 64 + lane] = ls2[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int v = 0; v < WGN; ++v) {
+          const int w = wm * WGN + v;
+          s1 += xm[((w * TM + i) * 2) * 64 + lane];
+          s2 += xm[((w * TM + i) * 2 + 1) * 64 + lane];
+        }
+        ls1[i] = s1;
+        ls2[i] = s2;
+      }
+    }
     // Row moments -> acc = rstd * (acc - mean * cs[n]), the LN'd-input GEMM before its bias.
     const float inv_n = 1.f / (float)a.lnf_n;
     float mu[TM], rs[TM];
