@@ -312,19 +312,22 @@ struct LaCfg {
   static constexpr int QV = C / 4 / VE;                  // x vectors per thread (4 thr / px)
   static constexpr bool WREG = ES == 2 && C <= 128;      // weights cached in registers (C = 256: L2)
   static constexpr int SMEM = 2 * XT + 4 * 64 * 4;      // x tiles + per-wave rescale scratch
-  // x tile slot swizzle and the slot of loader vector j of thread qq (4 threads per pixel). Both
-  // sides have to be conflict-free: the {lr, lg} ds_read_b128 fragment reads (16 rows from a
-  // multiple of 16) and the ds_write_b128 stores (8 lanes = 2 pixels x 4 threads per group, banks
-  // mod 32). 16-bit tiles: 128-byte rows f = row & 7 with vectors qq*QV + j; 256/512-byte rows
-  // f = 6 row mod SL with vectors j*4 + qq (found by enumerating both patterns; the earlier
-  // (row >> 1) & 7 and row & 15 stored 2-way (C = 64, 128) and 4-way (C = 256) conflicted:
-  // SQ_LDS_BANK_CONFLICT 20 % / 21 % / 47 % of the LDS cycles).
+  // x tile slot swizzle; thread qq of a pixel holds its 16-byte vectors qq*QV .. qq*QV + QV-1.
+  // Both sides have to be conflict-free: the {lr, lg} ds_read_b128 fragment reads (16 rows from
+  // a multiple of 16) and the ds_write_b128 stores (8 lanes = 2 pixels x 4 threads per group,
+  // banks mod 32). 16-bit tiles: 128-byte rows s ^ (row & 7); 256/512-byte rows also fold bits
+  // 3-4 of the slot into bits 1-2 before the row XOR, so a store's four slots qq*QV + j land on
+  // distinct bank groups (found by enumerating both patterns; the earlier (row >> 1) & 7 and
+  // row & 15 stored 2-way (C = 64, 128) and 4-way (C = 256) conflicted: SQ_LDS_BANK_CONFLICT
+  // 20 % / 21 % / 47 % of the LDS cycles). Layout only: each thread keeps its channels, so its
+  // LayerNorm sums are unchanged.
   DEV static int swz(int row, int s) {
-    const int f = ES == 2 ? (SL == 8 ? (row & 7) : ((row * 6) & (SL - 1)))
+    const int f = ES == 2 ? (SL == 8 ? (row & 7) : (row & 15))
                           : SL >= 16 ? (row & 15) : SL == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
-    return row * RB + ((s ^ f) << 4);
+    const int sp = ES == 2 && SL >= 16 ? s ^ (((s >> 3) & 3) << 1) : s;
+    return row * RB + ((sp ^ f) << 4);
   }
-  DEV static int vslot(int qq, int j) { return ES == 2 && SL >= 16 ? j * 4 + qq : qq * QV + j; }
+  DEV static int vslot(int qq, int j) { return qq * QV + j; }
 };
 
 // 16 bytes of MFMA operand (8 bf16 or 4 f32) assembled element by element.
