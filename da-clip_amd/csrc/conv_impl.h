@@ -1044,22 +1044,31 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv3_kernel(ConvArgs a, int R
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const EpiTerms<TN> et = epi_terms<TN>(a, n0, b, wn * WTN);   // latency hidden by the K loop
 
+  // One stage: 3 KSTEPS fragment groups (kw, ks). Group g + 1's fragments are read into the other
+  // register set before group g's MFMAs, so each group's LDS latency hides behind the previous
+  // group's MFMAs (read-then-use inside a group left ~4 MFMAs between a read and its first use:
+  // SQ_WAIT_INST_ANY 35 % of wave cycles at two waves per SIMD).
   auto compute = [&](int buf) {
     const char* st = smem + buf * STAGE;
+    constexpr int NG = 3 * KSTEPS;
+    u32x4 fa[2][TM], fb[2][TN];
+    auto load = [&](int g, int h) __attribute__((always_inline)) {
+      const int kw = g / KSTEPS, ks = g % KSTEPS;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
+      for (int i = 0; i < TM; ++i) fa[h][i] = *reinterpret_cast<const u32x4*>(st + aoff[i][kw][ks]);
 #pragma unroll
-      for (int ks = 0; ks < KSTEPS; ++ks) {
-        u32x4 fa[TM], fb[TN];
+      for (int jn = 0; jn < TN; ++jn) fb[h][jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
+    };
+    load(0, 0);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const u32x4*>(st + aoff[i][kw][ks]);
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) load(g + 1, (g + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);           // keep the reads ahead of this group's MFMAs
 #pragma unroll
-        for (int jn = 0; jn < TN; ++jn) fb[jn] = *reinterpret_cast<const u32x4*>(st + boff[kw][jn][ks]);
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[i], fb[jn]);
-      }
+        for (int jn = 0; jn < TN; ++jn) Mma<T>::run(acc[i][jn], fa[g & 1][i], fb[g & 1][jn]);
+    }
   };
   auto sync_stage = [&]() {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
