@@ -249,6 +249,39 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
       for (int j = 0; j < JT; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (CIN == 128) {
+        // Fragment groups (kh, c32) software-pipelined: group gg + 1's six interior fragments are
+        // read into the other register set before group gg's MFMAs, so the reads' LDS latency
+        // hides behind MFMAs instead of being waited out ~70 times a step (block1 is the block's critical path: 180 MFMAs per step against
+        // block2's 88). Same MFMAs in the same order per accumulator: bit-identical. (Cin 64's
+        // JT = 2 weight slice leaves no VGPRs for the second set.)
+        constexpr int NGR = 3 * NC1;
+        u32x4 F2[2][6];
+        auto gsrc = [&](int gg) { return xslot(t + gg / NC1 - 1) + ((gg % NC1) >> 1) * G::XHALF; };
+        auto ldF = [&](int gg, int h) __attribute__((always_inline)) {
+          const char* hr = gsrc(gg);
+          const int c = (gg % NC1) & 1;
+#pragma unroll
+          for (int s = 0; s < 6; ++s) F2[h][s] = *reinterpret_cast<const u32x4*>(hr + fo[c][s]);
+        };
+        ldF(0, 0);
+#pragma unroll
+        for (int gg = 0; gg < NGR; ++gg) {
+          const int kh = gg / NC1, c32 = gg % NC1, c = c32 & 1;
+          const char* hr = gsrc(gg);
+          if (gg + 1 < NGR) ldF(gg + 1, (gg + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Mma<T>::run(acc[i][0], W[(kh * 3 + kw) * NC1 + c32][0], F2[gg & 1][i + kw]);
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (eoff[kw] ^ (c << 6)));
+            Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][0], E);
+          }
+        }
+      } else {
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const char* xr = xslot(t + kh - 1);
@@ -275,6 +308,7 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
             }
           }
         }
+      }
       }
       __builtin_amdgcn_sched_barrier(0);
       // Epilogue -> LDS: h (scale / shift, SiLU) at halo pixel 64 g + 4 lr + i + 1; the lane's
