@@ -282,33 +282,56 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
           }
         }
       } else {
+        // Cin 64 (JT = 2): no VGPRs for a second fragment set, so the one set rolls: the group's
+        // MFMAs run in anti-diagonal order (fragment i + kw ascending; each accumulator still sums
+        // kw = 0, 1, 2 in order: bit-identical), F0..F2 die after the first half and take the next
+        // group's F0..F2, F3..F5 the next group's F3..F5 after the second half.
+        constexpr int NGR = 3 * NC1;
+        auto gsrc = [&](int gg) { return xslot(t + gg / NC1 - 1) + ((gg % NC1) >> 1) * G::XHALF; };
+        u32x4 F[6];
+        {
+          const char* hr0 = gsrc(0);
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const char* xr = xslot(t + kh - 1);
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr0 + fo[0][s]);
+        }
+        // (i, kw) pairs of the two halves: fragment i + kw <= 2, then >= 3.
+        constexpr int H1[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+        constexpr int H2[6][2] = {{1, 2}, {2, 1}, {3, 0}, {2, 2}, {3, 1}, {3, 2}};
 #pragma unroll
-        for (int c32 = 0; c32 < NC1; ++c32) {
+        for (int gg = 0; gg < NGR; ++gg) {
+          const int kh = gg / NC1, c32 = gg % NC1, c = c32 & 1;
+          const char* hr = gsrc(gg);
+          const char* hn = gsrc(gg + 1 < NGR ? gg + 1 : gg);
+          const int cn = ((gg + 1) % NC1) & 1;
           __builtin_amdgcn_sched_barrier(0);
-          const char* hr = xr + (c32 >> 1) * G::XHALF;
-          const int c = c32 & 1;
-          u32x4 F[6];
 #pragma unroll
-          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + fo[c][s]);
+          for (int q = 0; q < 6; ++q)
 #pragma unroll
-          for (int kw = 0; kw < 3; ++kw)
+            for (int j = 0; j < JT; ++j)
+              Mma<T>::run(acc[H1[q][0]][j], W[(kh * 3 + H1[q][1]) * NC1 + c32][j], F[H1[q][0] + H1[q][1]]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (gg + 1 < NGR) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int s = 0; s < 3; ++s) F[s] = *reinterpret_cast<const u32x4*>(hn + fo[cn][s]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-              for (int j = 0; j < JT; ++j) Mma<T>::run(acc[i][j], W[(kh * 3 + kw) * NC1 + c32][j], F[i + kw]);
-          {
+          for (int q = 0; q < 6; ++q)
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-              const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (eoff[kw] ^ (c << 6)));
-              if (JT == 1 || g == 0) Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][0], E);
-              else Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][JT - 1], E);
-            }
+            for (int j = 0; j < JT; ++j)
+              Mma<T>::run(acc[H2[q][0]][j], W[(kh * 3 + H2[q][1]) * NC1 + c32][j], F[H2[q][0] + H2[q][1]]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (gg + 1 < NGR) {
+#pragma unroll
+            for (int s = 3; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hn + fo[cn][s]);
+          }
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const u32x4 E = *reinterpret_cast<const u32x4*>(hr + (eoff[kw] ^ (c << 6)));
+            if (JT == 1 || g == 0) Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][0], E);
+            else Mma<T>::run(acce, W[(kh * 3 + kw) * NC1 + c32][JT - 1], E);
           }
         }
-      }
       }
       __builtin_amdgcn_sched_barrier(0);
       // Epilogue -> LDS: h (scale / shift, SiLU) at halo pixel 64 g + 4 lr + i + 1; the lane's
@@ -386,21 +409,45 @@ __global__ void __launch_bounds__(512, 2) rbfuse_kernel(RbArgs a, int RB) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < JT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+        // Groups (kh, c) with the rolling fragment set of block1's Cin 64 form (anti-diagonal
+        // MFMA order, each accumulator still kw = 0, 1, 2: bit-identical): the next group's
+        // F0..F2 / F3..F5 are read as soon as this group's uses of them are issued.
+        auto hsrc = [&](int gg) { return hring + ((u + gg / 2 - 1) & 3) * G::HROW; };
+        constexpr int H1[6][2] = {{0, 0}, {0, 1}, {1, 0}, {0, 2}, {1, 1}, {2, 0}};
+        constexpr int H2[6][2] = {{1, 2}, {2, 1}, {3, 0}, {2, 2}, {3, 1}, {3, 2}};
+        u32x4 F[6];
+        {
+          const char* h0 = hsrc(0);
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const char* hr = hring + ((u + kh - 1) & 3) * G::HROW;
+          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(h0 + fo[0][s]);
+        }
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int gg = 0; gg < 6; ++gg) {
+          const int kh = gg / 2, c = gg & 1, cn = (gg + 1) & 1;
+          const char* hn = hsrc(gg + 1 < 6 ? gg + 1 : gg);
           __builtin_amdgcn_sched_barrier(0);
-          u32x4 F[6];
 #pragma unroll
-          for (int s = 0; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hr + fo[c][s]);
+          for (int q = 0; q < 6; ++q)
 #pragma unroll
-          for (int kw = 0; kw < 3; ++kw)
+            for (int j = 0; j < JT; ++j)
+              Mma<T>::run(acc[H1[q][0]][j], W[(kh * 3 + H1[q][1]) * 2 + c][j], F[H1[q][0] + H1[q][1]]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (gg + 1 < 6) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int s = 0; s < 3; ++s) F[s] = *reinterpret_cast<const u32x4*>(hn + fo[cn][s]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-              for (int j = 0; j < JT; ++j) Mma<T>::run(acc[i][j], W[(kh * 3 + kw) * 2 + c][j], F[i + kw]);
+          for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int j = 0; j < JT; ++j)
+              Mma<T>::run(acc[H2[q][0]][j], W[(kh * 3 + H2[q][1]) * 2 + c][j], F[H2[q][0] + H2[q][1]]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (gg + 1 < 6) {
+#pragma unroll
+            for (int s = 3; s < 6; ++s) F[s] = *reinterpret_cast<const u32x4*>(hn + fo[cn][s]);
+          }
         }
       }
       // Cin 128: the 1x1 res_conv of x row u (still in the x ring; centre pixels, the same K order
