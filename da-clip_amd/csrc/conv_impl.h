@@ -692,6 +692,36 @@ __global__ void __launch_bounds__(64 * WGM * WGN) conv2_kernel(ConvArgs a) {
     if (kt == 0) DAC_ST(2, __builtin_amdgcn_s_memtime());
     const char* A = smem + (kt % STAGES) * STAGE;
     const char* Bs = A + BM * 128;
+    if constexpr (!GNA && !LNF && !SGEGLU && !(EPK & EPI_GEGLU) && !(BM == 256 && BN == 256) && STAGES > 1 && KSTEPS > 1) {
+      // Plain GEMMs: both k-steps' fragments are read into separate register sets before the
+      // tile's MFMAs, so a tile waits out one LDS latency instead of one per k-step (1 wave per
+      // SIMD in the 4-wave tiles: nothing else hides it). Same MFMAs in the same order:
+      // bit-identical. (The 256 x 256 tiles have no VGPRs to spare; the single-buffer K <= 64
+      // tiles measured slower with it, fewer blocks per CU.)
+      u32x4 pa[2][TM], pb[2][TN];
+      auto ld = [&](int ks, int h) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          pa[h][i] = *reinterpret_cast<const u32x4*>(A + swz(wm * WTM + i * 16 + lr, ks * 4 + lg));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          pb[h][j] = *reinterpret_cast<const u32x4*>(Bs + swz(wn * WTN + j * 16 + lr, ks * 4 + lg));
+      };
+      ld(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        if (ks + 1 < KSTEPS) ld(ks + 1, (ks + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (SWAP) Mma<T>::run(acc[i][j], pb[ks & 1][j], pa[ks & 1][i]);
+            else Mma<T>::run(acc[i][j], pa[ks & 1][i], pb[ks & 1][j]);
+          }
+      }
+      continue;
+    }
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       u32x4 fa[TM], fb[TN];
