@@ -819,7 +819,7 @@ void small_mha(const void* qkv, void* o, int B, int L, int H, int D, int causal,
   const dim3 g(H, B, (L + 63) / 64);
   if (D == 64) small_mha_kernel<T, 64><<<g, 256, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
   else if (D == 32) small_mha_kernel<T, 32><<<g, 256, smem, st>>>((const T*)qkv, (T*)o, L, H, causal);
-  else __builtin_trap();
+  else throw std::invalid_argument("small_mha: head dim must be 32 or 64");
 }
 
 template <typename T>

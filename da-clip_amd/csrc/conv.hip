@@ -274,7 +274,7 @@ void conv(const ConvArgs& a, int kh, int kw, int s, int p, hipStream_t st) {
   else if (kh == 7 && kw == 7 && s == 1 && p == 3) conv_dispatch<T, 7, 7, 1, 3>(a, st);
   else if (kh == 32 && kw == 32 && s == 32 && p == 0) conv_dispatch<T, 32, 32, 32, 0>(a, st);
   else if (kh == 14 && kw == 14 && s == 14 && p == 0) conv_dispatch<T, 14, 14, 14, 0>(a, st);
-  else __builtin_trap();
+  else throw std::invalid_argument("conv: unsupported kernel/stride/padding");
 }
 
 template void conv<float>(const ConvArgs&, int, int, int, int, hipStream_t);

@@ -2214,7 +2214,7 @@ void conv3w_launch(const ConvArgs& a, int delay, hipStream_t st) {
   const bool buf = buf_env && (a.C1 >= a.Cin || !a.x2 || a.ld2 == a.ld1) &&
                    (size_t)a.B * a.Hs * a.Ws * a.ld1 * 2 + a.ld1 * 2 < ((size_t)1 << 31);
   if (a.ys8) {                                      // fp8 output (conv_q8out_ok): buffer DMA form only
-    if (!buf) abort();
+    if (!buf) throw std::logic_error("conv3w: fp8 output needs the buffer-descriptor DMA form");
     conv3w_kernel<T, C3W_WAVES, 4, 2, true, true><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
   } else if (buf)
     conv3w_kernel<T, C3W_WAVES, 4, 2, true><<<conv3w_blocks(ntiles, C3W_WAVES), 64 * C3W_WAVES, 0, st>>>(a, ntiles, delay);
@@ -2247,7 +2247,8 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
   }
   // A fused second output is only requested after conv_res_fusable(a) said the v4 path takes it;
   // no path below may return without writing it.
-  if (a.y2 && !(KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2 && conv_res_fusable(a))) abort();
+  if (a.y2 && !(KH == 3 && KW == 3 && S == 1 && P == 1 && sizeof(T) == 2 && conv_res_fusable(a)))
+    throw std::logic_error("conv: fused second output requested on a shape without a fusing kernel");
   const int M = a.B * a.Ho * a.Wo;
   const bool batched = a.w_bstride > 0;
   const int Mg = batched ? a.Ho * a.Wo : M;
@@ -2321,7 +2322,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
     }
     // cwrap = 1 here means the row-tap dual layout (kernel rows wrap); the generic loaders read
     // a nonzero cwrap as a channel wrap instead, so no other kernel may take it.
-    if (a.cwrap) abort();
+    if (a.cwrap) throw std::logic_error("conv: 7x7 row-tap dual layout without its kernel");
   }
   if constexpr (KH == 3 && KW == 3 && S == 1 && P == 1) {
     const int RW = conv3_rw(a);
@@ -2345,19 +2346,19 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
             if (a.uph == 2 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192 | 16384>(a, st)) return;
             if (a.uph == 1 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 1024 | 8192>(a, st)) return;
             if (a.uph == 1 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 8192>(a, st)) return;
-            abort();
+            throw std::logic_error("conv: row-phase upsample conv without a matching v4 tile");
           }
           if (a.ys8) {                                // fp8 output (conv_q8out_ok): fused-res tiles only
             if (a.y2 && a.Cout == 64 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024 | 4096>(a, st)) return;
             if (a.y2 && a.Cout == 64 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 4096>(a, st)) return;
-            abort();
+            throw std::logic_error("conv: fp8 output without a matching fused v4 tile");
           }
           if (a.y2) {
             if (a.Cout % 64 == 0 && nb && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 256, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
             if (a.Cout % 64 == 0 && nb && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16 | 1024>(a, st)) return;
             if (a.Cout % 64 == 0 && conv3i_try<T, 128, 64, 4, 1, 64, 2, 12 | 16>(a, st)) return;
-            abort();                                  // conv_res_fusable promised a fused kernel
+            throw std::logic_error("conv: conv_res_fusable promised a fused kernel");
           } else if (a.Cout % 64 == 0 && nb && c3i_small_st(a, 256) == 3 && conv3i_try<T, 256, 64, 4, 1, 64, 3, 12 | 1024>(a, st)) {
             return;
           } else if (a.Cout % 64 == 0 && nb && c3i_small_st(a, 256) == 4 && conv3i_try<T, 256, 64, 4, 1, 64, 4, 12 | 1024>(a, st)) {
@@ -2449,7 +2450,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
         conv2_kernel<T, 128, 128, 2, 2, 2, KH, KW, S, P, EPI_LN><<<g, 256, 0, st>>>(a);
         return;
       }
-      __builtin_trap();                          // the engine only asks for these shapes
+      throw std::logic_error("conv: shape the engine never requests");
     }
     if constexpr (KH == 1) if (a.gna_stats) {
       // Input GroupNorm in the A path (conv_gna_ok mirrors this choice).
@@ -2459,7 +2460,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
           conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_SWAP | EPI_GNA><<<g, 256, 0, st>>>(a);
           return;
         }
-      __builtin_trap();
+      throw std::logic_error("conv: conv_gna_ok promised an input-GroupNorm kernel");
     }
     if constexpr (KH == 1) if (a.lnf_cs) {
       // Input LayerNorm folded in (conv_lnf_ok mirrors these two choices).
@@ -2473,7 +2474,7 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
           return;
         }
       }
-      __builtin_trap();                          // conv_lnf_ok said a folding kernel takes it
+      throw std::logic_error("conv: conv_lnf_ok promised a folding kernel");
     }
     const int f2 = (KH == 1 && g_conv2_force32 > 0 && a.Ho > 1 && a.Wo > 1 && a.Ho * a.Wo <= 1024 && a.Ho * a.Wo >= 256 && a.ksplit <= 1 && a.act != ACT_GEGLU) ? g_conv2_force32 : g_conv2_force;
     if constexpr (KH == 1) if (f2 > 0) {
@@ -2531,7 +2532,8 @@ void conv_dispatch(const ConvArgs& a0, hipStream_t st) {
     }
     if constexpr (KH == 1) if (a.ksplit > 1 && a.part) {
       // Split-K (conv_split_ok): 64x128 tiles, grid z = ksplit, then the reduce + epilogue pass.
-      if (a.ln_g || a.lnf_cs || a.gna_stats || batched || a.act == ACT_GEGLU) __builtin_trap();
+      if (a.ln_g || a.lnf_cs || a.gna_stats || batched || a.act == ACT_GEGLU)
+        throw std::logic_error("conv: epilogue feature without a kernel for this shape");
       dim3 g((Mg + 63) / 64, (a.Cout + 127) / 128, a.ksplit);
       conv2_kernel<T, 64, 128, 2, 2, 2, KH, KW, S, P, EPI_PART><<<g, 256, 0, st>>>(a);
       conv_part_reduce<T>(a, st);

@@ -971,7 +971,7 @@ void linear_attention_fused(const void* x, const void* wqkv, const float* wout, 
   else if constexpr (sizeof(T) == 2)
     la_proj_ctx<T, 256><<<dim3(nc, B), 256, 0, st>>>((const T*)x, (const T*)wqkv, part, HW, nc, CH, 1e-5f, la_tau());
   else
-    __builtin_trap();
+    throw std::invalid_argument("linear attention: fp32 path supports C = 64 or 128");
   // f16: W_eff ~ |Wout ctx| / HW sits in fp16's subnormal range (~1e-5 at 256^2), so it is
   // stored without the 1/HW and la_apply applies it to the fp32 accumulators (wscale).
   const float inv_hw = 1.f / (float)HW;
