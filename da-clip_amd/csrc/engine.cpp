@@ -201,11 +201,17 @@ static int wround_mode() {
   static const int m = getenv("DAC_WROUND") ? env_mask("DAC_WROUND") : 1;   // default: sum-keeping
   return m;
 }
+// DAC_WROUND_KEY=<substring>: sum-keeping rounding for the conv weights whose state-dict key
+// contains it, whatever DAC_WROUND says for the rest (a per-layer precision probe).
+static bool wround_key(const std::string& key) {
+  static const char* k = getenv("DAC_WROUND_KEY");
+  return k && *k && !key.empty() && key.find(k) != std::string::npos;
+}
 template <class C>
-static std::vector<uint16_t> quantize16(const std::vector<float>& v, int taps, int cin) {
+static std::vector<uint16_t> quantize16(const std::vector<float>& v, int taps, int cin, bool keep_sums = false) {
   std::vector<uint16_t> h(v.size());
   for (size_t i = 0; i < v.size(); ++i) h[i] = C::enc(v[i]);
-  const int m = wround_mode();
+  const int m = keep_sums ? 2 : wround_mode();
   if (taps < 2 || m == 0 || (m == 1 && C::kHalf)) return h;
   const size_t rows = v.size() / ((size_t)taps * cin);
   std::vector<size_t> idx(taps);
@@ -370,7 +376,7 @@ struct Packer {
       for (size_t i = 0; i < v.size(); ++i) q[i] = bf2f_host(h[i]);
       return pool.upload(q.data(), q.size() * 4);
     }
-    const std::vector<uint16_t> h = quantize16<typename CodecOf<T>::type>(v, taps, cin);
+    const std::vector<uint16_t> h = quantize16<typename CodecOf<T>::type>(v, taps, cin, wround_key(key));
     return pool.upload(h.data(), h.size() * 2);
   }
   const float* f32(const std::string& key, std::vector<int64_t> shape) {
