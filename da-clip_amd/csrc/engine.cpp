@@ -1472,12 +1472,15 @@ struct UNetNet {
   }
 
   // One forward. ss: [B][ss_total] of this step; out: [B*Hp*Wp][ldo] (channels < out_nc).
+  // prepped: the input rows are already in place (the previous loop step's sde_step wrote them
+  // at the same arena address, the first allocation after the reset); *xin_at receives it.
   void forward(Run& r, const float* xt, const float* mu, int B, int H, int W, const float* ss,
-               const float* cc, void* out, int ldo) {
+               const float* cc, void* out, int ldo, bool prepped = false, void** xin_at = nullptr) {
     const int Hp = pad_of(H), Wp = pad_of(W);
     const size_t M0 = (size_t)B * Hp * Wp;
     T* xin = r.alloc<T>(M0 * 8);
-    if (!r.dry) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
+    if (xin_at) *xin_at = xin;
+    if (!r.dry && !prepped) unet_prep<T>(xt, mu, xin, B, H, W, Hp, Wp, r.st);
     T* x0 = r.alloc<T>(M0 * nf);
     // Roles are assigned per section below; this scope restores the caller's role when the
     // forward returns (ViT / encoder calls on the thread are unaffected).
@@ -2028,14 +2031,19 @@ class EngineT : public Engine {
     unet->tables(r, b.sin, nT, (double)nT, -1.0, sched.time_scale, has_tc ? b.tcs : nullptr,
                  has_ic ? b.ics : nullptr, B, b.ss, b.cc);
     const size_t n = (size_t)B * 3 * H * W;
+    // Unpadded images: each step's sampler update also writes the next step's UNet input rows
+    // (same values unet_prep computes from the new x), one launch less per step.
+    static const bool fuse_prep = !getenv("DAC_FUSE_PREP") || atoi(getenv("DAC_FUSE_PREP")) != 0;
+    const bool fuse = fuse_prep && Hp == H && Wp == W && b.ldo >= 3;
     for (int i = 0; i < nT; ++i) {
       const int t = nT - i;
       r.ar->reset();
+      void* xin = nullptr;
       unet->forward(r, b.xs, b.mus, B, H, W, b.ss + (size_t)i * B * unet->ss_total, has_ic ? b.cc : nullptr,
-                    b.out, b.ldo);
+                    b.out, b.ldo, fuse && i > 0, &xin);
       if (!r.dry)
         sde_step<T>(mode, b.xs, b.mus, b.out, b.ldo, Hp, Wp, has_noise ? b.noise + (size_t)i * n : nullptr,
-                    b.seed, (uint32_t)t, sched.coef(t, mode), B, H, W, r.st);
+                    b.seed, (uint32_t)t, sched.coef(t, mode), B, H, W, r.st, fuse && i + 1 < nT ? xin : nullptr);
     }
   }
   void sde_reverse(int mode, float* x, const float* mu, const float* tc, const float* icx, int B,

@@ -308,11 +308,13 @@ void unet_out(const void* y, int ld, float* eps, int B, int H, int W, int Hp, in
 
 // Sampler updates on NCHW fp32 state (sde_utils.py:205-231, 245-247 / 44-45, 177-187).
 // eps is the padded NHWC model output. z: explicit noise or null -> Philox(*seedp, tag).
+// xin (loop form only, unpadded images): also write the next step's UNet input there, exactly
+// as unet_prep would from the new x (so the next forward skips its unet_prep launch).
 struct StepCoef { float sbar, ea, t1, t2, std, theta, sigma2, dt, sigma_sqrt_dt; };
 template <typename T>
 void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
               const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
-              int W, hipStream_t st);
+              int W, hipStream_t st, void* xin = nullptr);
 
 // ViT input: NCHW fp32 image -> NHWC T with channels padded to VE.
 template <typename T>

@@ -277,7 +277,7 @@ __global__ void sde_step_kernel(int mode, float* x, const float* mu, const T* ep
 template <typename T>
 __global__ void sde_step_px_kernel(int mode, float* x, const float* mu, const T* eps, int ld, int Hp,
                                    int Wp, const float* z, const uint64_t* seedp, uint32_t tag,
-                                   StepCoef c, int H, int W, size_t npx) {
+                                   StepCoef c, int H, int W, size_t npx, T* xin) {
   const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= npx) return;
   const int w = (int)(p % W);
@@ -288,6 +288,8 @@ __global__ void sde_step_px_kernel(int mode, float* x, const float* mu, const T*
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) e3[ch] = to_f(ep[ch]);
   const size_t plane = (size_t)H * W;
+  float v[8];                                   // next step's input row (unet_prep_kernel's)
+  v[6] = v[7] = 0.f;
 #pragma unroll
   for (int ch = 0; ch < 3; ++ch) {
     const size_t i = ((size_t)b * 3 + ch) * plane + (size_t)h * W + w;
@@ -305,19 +307,28 @@ __global__ void sde_step_px_kernel(int mode, float* x, const float* mu, const T*
       out = xv - drift - c.sigma_sqrt_dt * zv;                              // :44-45, 183-184
     }
     x[i] = out;
+    v[ch] = out - m;
+    v[3 + ch] = m;
+  }
+  if (xin) {                                    // (Hp == H, Wp == W: pixel p is input row p)
+    T* dst = xin + p * 8;
+    store_vec<T>(dst, v);
+    if constexpr (sizeof(T) == 4) store_vec<T>(dst + 4, v + 4);
   }
 }
 
 template <typename T>
 void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
               const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
-              int W, hipStream_t st) {
+              int W, hipStream_t st, void* xin) {
+  if (xin && (ld < 3 || Hp != H || Wp != W)) throw std::invalid_argument("sde_step: fused input write needs the unpadded loop form");
   if (ld >= 3 && !(getenv("DAC_SDE_PX") && atoi(getenv("DAC_SDE_PX")) == 0)) {
     const size_t npx = (size_t)B * H * W;
     sde_step_px_kernel<T><<<(unsigned)((npx + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld, Hp, Wp,
-                                                                         z, seedp, tag, c, H, W, npx);
+                                                                         z, seedp, tag, c, H, W, npx, (T*)xin);
     return;
   }
+  if (xin) throw std::invalid_argument("sde_step: fused input write needs the per-pixel kernel");
   const size_t n = (size_t)B * 3 * H * W;
   sde_step_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld,
                                                                   Hp, Wp, z, seedp, tag, c, H, W, n);
@@ -405,7 +416,7 @@ void rows_to_f32(const void* x, int ld, float* y, int R, int D, hipStream_t st) 
   template void unet_out<T>(const void*, int, float*, int, int, int, int, int, hipStream_t);  \
   template void sde_step<T>(int, float*, const float*, const void*, int, int, int,            \
                             const float*, const uint64_t*, uint32_t, StepCoef, int, int, int, \
-                            hipStream_t);                                                     \
+                            hipStream_t, void*);                                              \
   template void vit_prep<T>(const float*, void*, int, int, hipStream_t);                      \
   template void vit_patches<T>(const float*, void*, int, int, int, hipStream_t);               \
   template void vit_embed<T>(const void*, const float*, const float*, void*, int, int, int,   \
