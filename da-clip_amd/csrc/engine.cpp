@@ -2033,8 +2033,8 @@ class EngineT : public Engine {
     const size_t n = (size_t)B * 3 * H * W;
     // Unpadded images: each step's sampler update also writes the next step's UNet input rows
     // (same values unet_prep computes from the new x), one launch less per step.
-    static const bool fuse_prep = !getenv("DAC_FUSE_PREP") || atoi(getenv("DAC_FUSE_PREP")) != 0;
-    const bool fuse = fuse_prep && Hp == H && Wp == W && b.ldo >= 3;
+    const bool fuse_prep = !getenv("DAC_FUSE_PREP") || atoi(getenv("DAC_FUSE_PREP")) != 0;   // per recording
+    const bool fuse = fuse_prep && sde_step_fuses(b.ldo, H, W, Hp, Wp);
     for (int i = 0; i < nT; ++i) {
       const int t = nT - i;
       r.ar->reset();

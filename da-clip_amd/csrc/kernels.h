@@ -315,6 +315,8 @@ template <typename T>
 void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
               const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
               int W, hipStream_t st, void* xin = nullptr);
+// Whether sde_step can take xin for this layout (the per-pixel kernel on unpadded images).
+bool sde_step_fuses(int ld, int H, int W, int Hp, int Wp);
 
 // ViT input: NCHW fp32 image -> NHWC T with channels padded to VE.
 template <typename T>

@@ -317,18 +317,22 @@ __global__ void sde_step_px_kernel(int mode, float* x, const float* mu, const T*
   }
 }
 
+static bool sde_px_on() {                       // read per call: tests toggle it per handle
+  return !(getenv("DAC_SDE_PX") && atoi(getenv("DAC_SDE_PX")) == 0);
+}
+bool sde_step_fuses(int ld, int H, int W, int Hp, int Wp) { return sde_px_on() && ld >= 3 && Hp == H && Wp == W; }
+
 template <typename T>
 void sde_step(int mode, float* x, const float* mu, const void* eps, int ld, int Hp, int Wp,
               const float* z, const uint64_t* seedp, uint32_t tag, StepCoef c, int B, int H,
               int W, hipStream_t st, void* xin) {
-  if (xin && (ld < 3 || Hp != H || Wp != W)) throw std::invalid_argument("sde_step: fused input write needs the unpadded loop form");
-  if (ld >= 3 && !(getenv("DAC_SDE_PX") && atoi(getenv("DAC_SDE_PX")) == 0)) {
+  if (xin && !sde_step_fuses(ld, H, W, Hp, Wp)) throw std::invalid_argument("sde_step: fused input write needs the per-pixel kernel on unpadded images");
+  if (ld >= 3 && sde_px_on()) {
     const size_t npx = (size_t)B * H * W;
     sde_step_px_kernel<T><<<(unsigned)((npx + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld, Hp, Wp,
                                                                          z, seedp, tag, c, H, W, npx, (T*)xin);
     return;
   }
-  if (xin) throw std::invalid_argument("sde_step: fused input write needs the per-pixel kernel");
   const size_t n = (size_t)B * 3 * H * W;
   sde_step_kernel<T><<<(unsigned)((n + 255) / 256), 256, 0, st>>>(mode, x, mu, (const T*)eps, ld,
                                                                   Hp, Wp, z, seedp, tag, c, H, W, n);

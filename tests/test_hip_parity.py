@@ -119,6 +119,12 @@ def test_loop_sde_step_pixel_kernel_bit_identical(unet_sd, monkeypatch, mode):
     px = run()
     assert torch.isfinite(px).all()
     assert torch.equal(px, planar)
+    # The per-pixel kernel also writes the next step's UNet input (unet_prep skipped); without
+    # that fusion the loop must give the same bits.
+    monkeypatch.setenv("DAC_FUSE_PREP", "0")
+    unfused = run()
+    monkeypatch.delenv("DAC_FUSE_PREP")
+    assert torch.equal(px, unfused)
 
 
 def test_unet_batch8_matches_single_image_fp16(unet_sd):
