@@ -1,5 +1,5 @@
 # (Removed experiment: no gain; DESIGN.md §9. The two-tile form is not in conv_edge.hip.)
-# conv7 (init conv) with two channel tiles per wave (each LDS pixel fragment feeds two MFMAs)
+# conv7 (init conv) variants against libab/base.so / libab/convbench_base:
 # against libab/base.so / libab/convbench_base: op-level check + time, in-graph times, equal PSNR.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
